@@ -1,0 +1,25 @@
+# Builds the C-ABI library mepol_amd/libmepol_amd.so for gfx950 (MI355X) and the oracle's
+# optional C helpers.  `make -j8` here; the .so travels to the GPU box with the snapshot.
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+FLAGS   := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
+SRC     := $(wildcard mepol_amd/csrc/*.hip)
+OBJ     := $(patsubst mepol_amd/csrc/%.hip,build/%.o,$(SRC))
+LIB     := mepol_amd/libmepol_amd.so
+
+all: $(LIB)
+
+build/%.o: mepol_amd/csrc/%.hip mepol_amd/csrc/common.hpp include/mepol_amd.h
+	@mkdir -p build
+	$(HIPCC) $(FLAGS) -Iinclude -c $< -o $@
+
+$(LIB): $(OBJ)
+	$(HIPCC) $(FLAGS) -shared -o $@ $(OBJ)
+
+resource-usage:
+	@for f in $(SRC); do $(HIPCC) $(FLAGS) -Iinclude -c $$f -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|Scratch|Occupancy"; done
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean resource-usage

@@ -1,0 +1,118 @@
+/* mepol_amd.h -- C ABI of the MI355X (gfx950) MEPOL hot path.
+ *
+ * The reference (RiccZamboni/mepol) is pure Python and has no FFI; these entry points are what
+ * its hot path (src/algorithms/mepol.py) binds to when it is switched to this library.  Each
+ * function names the reference interface it replaces.  The Python drop-in module
+ * (mepol_amd/algorithms/mepol.py) calls them through ctypes (mepol_amd/_lib.py); the binding a
+ * maintainer would add to the reference is shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - All array arguments are DEVICE pointers owned by the caller (e.g. torch tensors via
+ *    data_ptr()); nothing is allocated inside a call.  Scratch comes from a caller-owned
+ *    workspace whose size the *_workspace_size query returns.
+ *  - `stream` is a hipStream_t; every call only enqueues work on it (no host sync), so calls
+ *    can be captured into a hipGraph.
+ *  - Return value: 0 on success, a hipError_t value or one of the MEPOL_ERR_* codes otherwise;
+ *    mepol_last_error_string() describes the last failure of the calling thread.
+ *  - Stateless and re-entrant; ordering comes from the stream.
+ *  - Particle indices are int32 on device (N < 2^31); the Python boundary widens them to the
+ *    reference's int64 where it returns them.
+ */
+#ifndef MEPOL_AMD_H
+#define MEPOL_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MEPOL_ERR_BAD_ARG 1001
+#define MEPOL_ERR_WORKSPACE 1002
+#define MEPOL_ERR_UNSUPPORTED 1003
+
+const char* mepol_last_error_string(void);
+int mepol_abi_version(void);
+
+/* ---- k-NN ---------------------------------------------------------------------------------
+ * Replaces src/algorithms/mepol.py:190-192
+ *     NearestNeighbors(n_neighbors=k+1, metric='euclidean', algorithm='auto', n_jobs=W)
+ *         .fit(next_states).kneighbors(next_states)
+ * cand [n_cand, d] f32 row-major, query [n_query, d] f32 (a shard of cand or cand itself).
+ * Outputs: dist_out [n_query, kp1] f64 = sqrt(sum_f (q_f - c_f)^2) in f64 (sklearn kd_tree's
+ * arithmetic), rows ascending, ties by smaller index; idx_out [n_query, kp1] int64 (nullable);
+ * idx32_out [kp1, n_query] int32 TRANSPOSED (nullable; the layout the entropy kernels read).
+ * n_fallback_out (nullable, device int32): number of queries answered by the exhaustive path.
+ * split_hint: 0 = automatic candidate split.  Fast path: d <= 63, kp1 <= 60. */
+int mepol_knn_workspace_size(int64_t n_cand, int64_t n_query, int d, int kp1, int split_hint,
+                             size_t* bytes);
+int mepol_knn_plan_info(int64_t n_cand, int64_t n_query, int d, int kp1, int split_hint, int* ks,
+                        int* list, int* split);
+int mepol_knn(const float* cand, int64_t n_cand, const float* query, int64_t n_query, int d,
+              int kp1, int split_hint, double* dist_out, int64_t* idx_out, int32_t* idx32_out,
+              int32_t* n_fallback_out, void* workspace, size_t workspace_bytes, void* stream);
+/* Exhaustive f64 scan for every query (kp1 <= 64); scratch_idx: int32 [1 + n_query]. */
+int mepol_knn_exact(const float* cand, int64_t n_cand, const float* query, int64_t n_query, int d,
+                    int kp1, double* dist_out, int64_t* idx_out, int32_t* idx32_out,
+                    int32_t* scratch_idx, void* stream);
+
+/* ---- importance weights -------------------------------------------------------------------
+ * Replaces compute_importance_weights, src/algorithms/mepol.py:114-139:
+ *   u[off[n]+t] = exp(cumsum_{s<=t}(logp_t - logp_b)[n, s]);  w = u / sum(u).
+ * logp_t/logp_b: [num_traj, T_stride] f64 (log-probs of target / behavioral policy);
+ * traj_offsets: [num_traj+1] int64 particle offsets (real trajectory lengths, mepol.py:122).
+ * traj_sum_out [num_traj]; w_out/U_out nullable (skip normalisation, e.g. multi-rank). */
+int mepol_iw_forward(const double* logp_t, const double* logp_b, int64_t num_traj,
+                     int64_t T_stride, const int64_t* traj_offsets, int64_t n_particles,
+                     double* u_out, double* traj_sum_out, double* w_out, double* U_out,
+                     void* stream);
+/* w = u / *U with a device scalar U (multi-rank: U all-reduced). */
+int mepol_iw_normalize(const double* u, const double* U, int64_t n, double* w, void* stream);
+
+/* ---- entropy / KL -------------------------------------------------------------------------
+ * Replaces compute_entropy (mepol.py:142-154) and compute_kl (mepol.py:157-174), fused:
+ *   W_i = sum_{c<k} w[I[i,c]];  V_i = D[i,k]^ns pi^(ns/2)/G;
+ *   out4[0] = H  = -sum_i (W_i/k) log(W_i/(V_i+eps)+eps) + B
+ *   out4[1] = KL = (1/n_w) sum_i log(k/(n_w W_i) + eps)     (before the max(0, .) clamp)
+ *   out4[2], out4[3] = the two raw sums (for cross-rank reduction).
+ * w [n_w] (global), idxT [kp1, n] int32, D [n, kp1] f64; W_out, g_out [n] (g = dH/dW);
+ * partials: [2 * mepol_entropy_partials_size(n)] f64 scratch. */
+int mepol_entropy_partials_size(int64_t n_particles);
+int mepol_entropy_forward(const double* w, const int32_t* idxT, const double* D, int64_t n,
+                          int64_t n_w, int k, int kp1, double ns, double G, double B, double eps,
+                          double* W_out, double* g_out, double* partials, double* out4,
+                          void* stream);
+
+/* ---- entropy gradient (the autograd of policy_update's loss.backward(), mepol.py:278) ----
+ * CSR transpose of the first k rows of idxT for owned ids [col_offset, col_offset + ncand). */
+int mepol_csr_build(const int32_t* idxT, int64_t nq, int k, int64_t col_offset, int64_t ncand,
+                    int64_t row_offset, int32_t* csr_off, int32_t* csr_rows, int32_t* scratch,
+                    void* stream);
+/* gamma_j = sum_{i in CSR(j)} g_i ; partials[b] = block sums of gamma_j w_j. */
+int mepol_entropy_gamma(const double* g, const double* w_own, const int32_t* csr_off,
+                        const int32_t* csr_rows, int64_t n_own, double* gamma_out,
+                        double* partials, void* stream);
+/* grad_logp[n, s] = grad_H * sum_{t>=s} (gamma_{n,t} - S) w_{n,t},  S = sum(partials) or *S_ext. */
+int mepol_entropy_reverse_scan(const double* gamma, const double* w, const double* partials,
+                               int64_t nparts, const double* S_ext, const int64_t* traj_offsets,
+                               int64_t num_traj, int64_t T_stride, const double* grad_H,
+                               double* grad_logp, void* stream);
+
+/* ---- environments -------------------------------------------------------------------------
+ * Replace MountainCarContinuous.step (src/envs/mountain_car_wall.py:13-45) and
+ * GridWorldContinuous.step (src/envs/gridworld_continuous.py:128-154), batched. */
+int mepol_step_mountaincar(double* state, const double* action, int64_t n, int64_t action_stride,
+                           void* stream);
+int mepol_step_gridworld(float* state, const double* action, int64_t n, void* stream);
+/* One step of collect_particles (mepol.py:81-90) for n trajectories: a = mean + noise*exp(log_std),
+ * record s_{t+1}/a_t as f32, advance the env. env_id 0 = MountainCar, 1 = GridWorld. */
+int mepol_rollout_step(int env_id, double* env_f64, float* env_f32, const double* mean,
+                       const double* noise, const double* log_std, int64_t n, int a_dim, int64_t t,
+                       int64_t T, float* states_rec, float* actions_rec, double* policy_in,
+                       void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MEPOL_AMD_H */

@@ -1,0 +1,521 @@
+"""MEPOL hot path on MI355X: drop-in for src/algorithms/mepol.py of the reference.
+
+Same function names, argument order/meaning and return types as the reference
+(src/algorithms/mepol.py), with the particle batch resident in HBM:
+
+  collect_particles(env, policy, num_traj, traj_len, state_filter)            :70-111
+  compute_importance_weights(behavioral, target, states, actions, nt, rtl)   :114-139
+  compute_entropy(..., distances, indices, k, G, B, ns, eps)                  :142-154
+  compute_kl(..., distances, indices, k, eps)                                 :157-174
+  collect_particles_and_compute_knn(env, policy, nt, T, state_filter, k, W)   :177-202
+  policy_update(optimizer, behavioral, target, ..., k, G, B, ns, eps)         :268-281
+  mepol(env, env_name, state_filter, create_policy, k, kl_threshold, ...)     :284-545
+
+Differences a caller can observe (all documented in DESIGN.md):
+  * tensors returned by collect_particles_and_compute_knn live on the GPU (the reference's
+    "#todo: any target device", mepol.py:194); collect_particles still returns numpy;
+  * k-NN ties are broken by the smaller index (sklearn's order is implementation-defined);
+  * rollout noise comes from torch's device generator, so trajectories are not the CPU
+    reference's random stream (dynamics are; see tests/test_gpu_envs.py).
+"""
+import math
+import os
+import time
+
+import numpy as np
+import scipy.special
+import torch
+
+from .. import ops
+from ..envs.wrappers import unwrap
+from . import particles as P
+
+float_type = torch.float64
+int_type = torch.int64
+
+
+# ---------------------------------------------------------------------------------------------
+# Rollout
+# ---------------------------------------------------------------------------------------------
+def _batched_kind(env):
+    return getattr(type(unwrap(env)), "batched_kind", None)
+
+
+def collect_particles_device(env, policy, num_traj, traj_len, state_filter, generator=None):
+    """Rollout of num_traj trajectories of traj_len steps, batched on the policy's device.
+
+    Returns device tensors: states f32 [nt, T+1, nf], actions f32 [nt, T, a], real lengths
+    int32 [nt, 1], next_states f32 [N, ns] (particle p = n*T + t <-> s_{n, t+1}, mepol.py:98-109).
+    MountainCar / GridWorld step in a HIP kernel (one fused launch per step after the MLP);
+    any other env is stepped on the host in lockstep with one batched policy call per step.
+    """
+    dev = policy.device
+    if dev.type != "cuda":
+        raise RuntimeError("collect_particles_device needs the policy on a ROCm device")
+    base = unwrap(env)
+    kind = _batched_kind(env)
+    nf = env.num_features
+    a_dim = env.action_space.shape[0]
+    T = int(traj_len)
+    states = torch.zeros((num_traj, T + 1, nf), dtype=torch.float32, device=dev)
+    actions = torch.zeros((num_traj, T, a_dim), dtype=torch.float32, device=dev)
+    with torch.no_grad():
+        if kind in ("mountaincar", "gridworld"):
+            env_id = 0 if kind == "mountaincar" else 1
+            init = base.reset_batch_torch(num_traj, dev, generator)
+            env64 = init.clone() if env_id == 0 else None
+            env32 = init.clone() if env_id == 1 else None
+            policy_in = init.to(torch.float64).contiguous()
+            states[:, 0] = init.to(torch.float32)
+            log_std = policy.log_std.detach().contiguous()
+            for t in range(T):
+                mean = policy.mean_action(policy_in).contiguous()
+                noise = torch.randn(mean.shape, dtype=torch.float64, device=dev,
+                                    generator=generator)
+                ops.rollout_step(env_id, env64, env32, mean, noise, log_std, t, T, states, actions,
+                                 policy_in)
+        else:
+            envs = [env] + [_clone_env(env) for _ in range(num_traj - 1)]
+            s = np.stack([e.reset() for e in envs])
+            states[:, 0] = torch.as_tensor(s, dtype=torch.float32, device=dev)
+            for t in range(T):
+                x = torch.as_tensor(s, dtype=torch.float64, device=dev)
+                _, a = policy(x)
+                actions[:, t] = a.to(torch.float32)
+                a_np = a.cpu().numpy()
+                s = np.stack([e.step(a_np[i])[0] for i, e in enumerate(envs)])
+                states[:, t + 1] = torch.as_tensor(s, dtype=torch.float32, device=dev)
+    rtl = torch.full((num_traj, 1), T, dtype=torch.int32, device=dev)
+    next_states = states[:, 1:, :].reshape(-1, nf)
+    if state_filter is not None:
+        next_states = next_states[:, list(state_filter)]
+    return states, actions, rtl, next_states.contiguous()
+
+
+def _clone_env(env):
+    import copy
+
+    return copy.deepcopy(env)
+
+
+def collect_particles(env, policy, num_traj, traj_len, state_filter):
+    """Reference signature (mepol.py:70-111): numpy f32 states/actions/next_states, i32 lengths."""
+    s, a, r, ns = collect_particles_device(env, policy, num_traj, traj_len, state_filter)
+    return s.cpu().numpy(), a.cpu().numpy(), r.cpu().numpy(), ns.cpu().numpy()
+
+
+def collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len, state_filter, k,
+                                      num_workers):
+    """Rollout + exact k-NN (mepol.py:177-202); tensors stay on the GPU.
+
+    num_workers keeps the reference's divisibility contract (mepol.py:179); the whole batch is
+    rolled out by the GPU, so no worker processes are spawned.
+    """
+    assert num_traj % num_workers == 0, "Please provide a number of trajectories " \
+                                        "that can be equally split among workers"
+    s32, a32, rtl32, ns32 = collect_particles_device(env, behavioral_policy, num_traj, traj_len,
+                                                     state_filter)
+    D, I, I32T = ops.knn(ns32, k + 1)
+    states = s32.to(float_type)
+    actions = a32.to(float_type)
+    next_states = ns32.to(float_type)
+    real_traj_lengths = rtl32.to(int_type)
+    batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T)
+    P.register(I, batch)
+    return states, actions, real_traj_lengths, next_states, D, I
+
+
+def make_particle_batch(states, actions, real_traj_lengths, next_states_f32, k):
+    """Register a batch built from externally produced particles (e.g. a MuJoCo rollout or a
+    synthetic benchmark batch): runs the GPU k-NN and returns the reference's 6-tuple."""
+    D, I, I32T = ops.knn(next_states_f32, k + 1)
+    batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T)
+    P.register(I, batch)
+    return states, actions, real_traj_lengths, next_states_f32.to(float_type), D, I
+
+
+# ---------------------------------------------------------------------------------------------
+# Importance weights / entropy / KL
+# ---------------------------------------------------------------------------------------------
+class _IWFunction(torch.autograd.Function):
+    """w = normalize(exp(segmented cumsum(logp_t - logp_b))) with its exact backward."""
+
+    @staticmethod
+    def forward(ctx, logp_t, logp_b, batch):
+        _, _, w, _ = ops.iw_forward(logp_t.detach(), logp_b.detach(), batch.offsets, batch.N)
+        ctx.batch = batch
+        ctx.save_for_backward(w)
+        return w
+
+    @staticmethod
+    def backward(ctx, grad_w):
+        (w,) = ctx.saved_tensors
+        b = ctx.batch
+        grad_w = grad_w.contiguous()
+        S = torch.dot(grad_w, w).reshape(())
+        one = torch.ones((), dtype=torch.float64, device=w.device)
+        grad = ops.entropy_reverse_scan(grad_w, w, S, 0, b.offsets, b.num_traj, b.T, one, S_ext=S)
+        return grad, None, None
+
+
+class _EntropyFunction(torch.autograd.Function):
+    """H(logp_t) of compute_entropy, fused with compute_kl's statistic (one forward).
+
+    forward: IW scan + normalise + gather/volume/log terms (HIP); saves w and dH/dW.
+    backward: CSR gather of dH/dW -> gamma, S = <gamma, w>, segmented reverse scan (HIP);
+    the result is dH/dlogp_t, which torch autograd pushes through the MLP.
+    """
+
+    @staticmethod
+    def forward(ctx, logp_t, logp_b, batch, k, G, B, ns, eps):
+        _, _, w, _ = ops.iw_forward(logp_t.detach(), logp_b.detach(), batch.offsets, batch.N)
+        out4, _, g = ops.entropy_forward(w, batch.idx32T, batch.D, k, ns, G, B, eps)
+        ctx.batch, ctx.k = batch, k
+        ctx.save_for_backward(w, g)
+        ctx.out4 = out4
+        ctx.mark_non_differentiable(out4)
+        return out4[0].clone(), out4
+
+    @staticmethod
+    def backward(ctx, grad_H, _grad_out4):
+        w, g = ctx.saved_tensors
+        b = ctx.batch
+        off, rows = b.csr(ctx.k)
+        gamma, partials, nparts = ops.entropy_gamma(g, w, off, rows)
+        gH = grad_H.reshape(()).to(torch.float64).contiguous()
+        grad = ops.entropy_reverse_scan(gamma, w, partials, nparts, b.offsets, b.num_traj, b.T, gH)
+        return grad, None, None, None, None, None, None, None
+
+
+def _logps(batch, behavioral_policy, target_policy):
+    logp_b = batch.behavioral_logp(behavioral_policy)
+    if target_policy is behavioral_policy:
+        return logp_b, logp_b
+    if torch.is_grad_enabled():
+        stashed = batch.take_logp(target_policy)
+        if stashed is not None:
+            return stashed, logp_b
+    return batch.logp(target_policy), logp_b
+
+
+def compute_importance_weights(behavioral_policy, target_policy, states, actions, num_traj,
+                               real_traj_lengths):
+    """Normalised per-particle importance weights w [N] f64 (mepol.py:114-139), differentiable
+    w.r.t. the target policy's parameters."""
+    batch = P.ParticleBatch(states, actions, real_traj_lengths,
+                            torch.zeros((1, 2), dtype=torch.float64),
+                            torch.zeros((1, 2), dtype=torch.int64))
+    logp_t, logp_b = _logps(batch, behavioral_policy, target_policy)
+    return _IWFunction.apply(logp_t, logp_b, batch)
+
+
+def compute_entropy(behavioral_policy, target_policy, states, actions, num_traj, real_traj_lengths,
+                    distances, indices, k, G, B, ns, eps):
+    """KL (Kozachenko-Leonenko) entropy estimate, 0-d f64 (mepol.py:142-154)."""
+    batch = P.lookup(states, actions, real_traj_lengths, distances, indices)
+    logp_t, logp_b = _logps(batch, behavioral_policy, target_policy)
+    H, _ = _EntropyFunction.apply(logp_t, logp_b, batch, k, G, B, ns, eps)
+    return H
+
+
+def compute_kl(behavioral_policy, target_policy, states, actions, num_traj, real_traj_lengths,
+               distances, indices, k, eps):
+    """k-NN KL(behavioral || target) estimate and its numeric-error flag (mepol.py:157-174).
+
+    When gradients are enabled, the target policy's MLP forward is kept (with its graph) so a
+    following policy_update at the same parameters reuses it instead of recomputing it; the
+    returned values are those of the reference's no_grad computation.
+    """
+    batch = P.lookup(states, actions, real_traj_lengths, distances, indices)
+    logp_b = batch.behavioral_logp(behavioral_policy)
+    if target_policy is behavioral_policy:
+        logp_t = logp_b
+    elif torch.is_grad_enabled() and any(p.requires_grad for p in target_policy.parameters()):
+        logp_t = batch.logp(target_policy)
+        batch.stash_logp(target_policy, logp_t)
+    else:
+        with torch.no_grad():
+            logp_t = batch.logp(target_policy)
+    with torch.no_grad():
+        _, _, w, _ = ops.iw_forward(logp_t.detach(), logp_b, batch.offsets, batch.N)
+        out4, _, _ = ops.entropy_forward(w, batch.idx32T, batch.D, k, 1.0, 1.0, 0.0, eps)
+    kl = out4[1].clone()
+    numeric_error = bool(torch.isinf(kl) or torch.isnan(kl))
+    kl = torch.clamp_min(kl, 0.0)
+    return kl, numeric_error
+
+
+def policy_update(optimizer, behavioral_policy, target_policy, states, actions, num_traj, traj_len,
+                  distances, indices, k, G, B, ns, eps):
+    """One gradient step maximising the entropy estimate (mepol.py:268-281).
+
+    The 5th positional argument is the real trajectory lengths, as at the reference call site
+    (mepol.py:429-431).
+    """
+    optimizer.zero_grad()
+    loss = -compute_entropy(behavioral_policy, target_policy, states, actions, num_traj, traj_len,
+                            distances, indices, k, G, B, ns, eps)
+    numeric_error = bool(torch.isinf(loss) or torch.isnan(loss))
+    loss.backward()
+    optimizer.step()
+    return loss, numeric_error
+
+
+# ---------------------------------------------------------------------------------------------
+# Logging (output formats of mepol.py:205-265)
+# ---------------------------------------------------------------------------------------------
+def _summary_writer(out_path):
+    try:
+        from torch.utils import tensorboard  # noqa: F401
+
+        return tensorboard.SummaryWriter(out_path)
+    except Exception:
+        class _Null:
+            def add_scalar(self, *a, **kw):
+                pass
+
+            def add_figure(self, *a, **kw):
+                pass
+
+        return _Null()
+
+
+def log_epoch_statistics(writer, log_file, csv_file_1, csv_file_2, epoch, loss, entropy,
+                         num_off_iters, execution_time, full_entropy, heatmap_image,
+                         heatmap_entropy, backtrack_iters, backtrack_lr):
+    writer.add_scalar("Loss", loss, global_step=epoch)
+    writer.add_scalar("Entropy", entropy, global_step=epoch)
+    writer.add_scalar("Execution time", execution_time, global_step=epoch)
+    writer.add_scalar("Number off-policy iteration", num_off_iters, global_step=epoch)
+    if full_entropy is not None:
+        writer.add_scalar("Full Entropy:", full_entropy, global_step=epoch)
+    rows = [["Epoch", epoch], ["Execution time (s)", f"{execution_time:.3f}"],
+            ["Entropy", f"{entropy:.3f}"], ["Off-policy iters", num_off_iters]]
+    if heatmap_image is not None:
+        rows.append(["Heatmap entropy", f"{heatmap_entropy:.3f}"])
+    if backtrack_iters is not None:
+        rows.append(["Backtrack iters", backtrack_iters])
+    try:
+        from tabulate import tabulate
+
+        grid = tabulate(rows, headers="firstrow", tablefmt="fancy_grid", numalign="right")
+    except ImportError:
+        grid = "\n".join(f"{a}: {b}" for a, b in rows)
+    csv_file_1.write(f"{epoch},{loss},{entropy},{full_entropy},{num_off_iters},{execution_time}\n")
+    csv_file_1.flush()
+    if heatmap_image is not None and csv_file_2 is not None:
+        csv_file_2.write(f"{epoch},{heatmap_entropy}\n")
+        csv_file_2.flush()
+    log_file.write(grid)
+    log_file.flush()
+    print(grid)
+
+
+def log_off_iter_statistics(writer, csv_file_3, epoch, global_off_iter, num_off_iter, entropy, kl,
+                            lr):
+    csv_file_3.write(f"{epoch},{num_off_iter},{entropy},{kl},{lr}\n")
+    csv_file_3.flush()
+    writer.add_scalar("Off policy iter Entropy", entropy, global_step=global_off_iter)
+    writer.add_scalar("Off policy iter KL", kl, global_step=global_off_iter)
+
+
+def _save_policy(policy, path):
+    torch.save({k: v.detach().cpu() for k, v in policy.state_dict().items()}, path)
+
+
+# ---------------------------------------------------------------------------------------------
+# Driver
+# ---------------------------------------------------------------------------------------------
+def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_iters,
+          use_backtracking, backtrack_coeff, max_backtrack_try, eps, learning_rate, num_traj,
+          traj_len, num_epochs, optimizer, full_entropy_traj_scale, full_entropy_k, heatmap_every,
+          heatmap_discretizer, heatmap_episodes, heatmap_num_steps, heatmap_cmap, heatmap_labels,
+          heatmap_interp, seed, out_path, num_workers):
+    """The MEPOL epoch loop (mepol.py:284-545) with the reference's control flow and outputs.
+
+    Heatmaps (mepol.py:19-67) are out of scope: a discretizer is accepted and ignored.
+    """
+    if seed is not None:
+        np.random.seed(seed)
+        torch.manual_seed(seed)
+        env.seed(seed)
+
+    behavioral_policy = create_policy(is_behavioral=True)
+    target_policy = create_policy()
+    last_valid_target_policy = create_policy()
+    target_policy.load_state_dict(behavioral_policy.state_dict())
+    last_valid_target_policy.load_state_dict(behavioral_policy.state_dict())
+
+    if optimizer == "rmsprop":
+        optimizer = torch.optim.RMSprop(target_policy.parameters(), lr=learning_rate)
+    elif optimizer == "adam":
+        optimizer = torch.optim.Adam(target_policy.parameters(), lr=learning_rate)
+    else:
+        raise NotImplementedError
+
+    writer = _summary_writer(out_path)
+    log_file = open(os.path.join(out_path, "log_file.txt"), "a", encoding="utf-8")
+    csv_file_1 = open(os.path.join(out_path, f"{env_name}.csv"), "w")
+    csv_file_1.write(",".join(["epoch", "loss", "entropy", "full_entropy", "num_off_iters",
+                               "execution_time"]))
+    csv_file_1.write("\n")
+    csv_file_2 = None
+    csv_file_3 = open(os.path.join(out_path, f"{env_name}_off_policy_iter.csv"), "w")
+    csv_file_3.write(",".join(["epoch", "off_policy_iter", "entropy", "kl", "learning_rate"]))
+    csv_file_3.write("\n")
+
+    ns = len(state_filter) if (state_filter is not None) else env.num_features
+    B = np.log(k) - scipy.special.digamma(k)
+    full_B = np.log(full_entropy_k) - scipy.special.digamma(full_entropy_k)
+    G = scipy.special.gamma(ns / 2 + 1)
+
+    epoch = 0
+    _sync()
+    t0 = time.time()
+    states, actions, real_traj_lengths, next_states, distances, indices = \
+        collect_particles_and_compute_knn(env, behavioral_policy, num_traj * full_entropy_traj_scale,
+                                          traj_len, state_filter, full_entropy_k, num_workers)
+    with torch.no_grad():
+        full_entropy = compute_entropy(behavioral_policy, behavioral_policy, states, actions,
+                                       num_traj * full_entropy_traj_scale, real_traj_lengths,
+                                       distances, indices, full_entropy_k, G, full_B, ns, eps)
+    states, actions, real_traj_lengths, next_states, distances, indices = \
+        collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len, state_filter,
+                                          k, num_workers)
+    with torch.no_grad():
+        entropy = compute_entropy(behavioral_policy, behavioral_policy, states, actions, num_traj,
+                                  real_traj_lengths, distances, indices, k, G, B, ns, eps)
+    full_entropy = _np(full_entropy)
+    entropy = _np(entropy)
+    execution_time = time.time() - t0
+    loss = -entropy
+    heatmap_entropy = None
+    heatmap_image = None
+    _save_policy(behavioral_policy, os.path.join(out_path, f"{epoch}-policy"))
+    log_epoch_statistics(writer=writer, log_file=log_file, csv_file_1=csv_file_1,
+                         csv_file_2=csv_file_2, epoch=epoch, loss=loss, entropy=entropy,
+                         execution_time=execution_time, num_off_iters=0, full_entropy=full_entropy,
+                         heatmap_image=heatmap_image, heatmap_entropy=heatmap_entropy,
+                         backtrack_iters=None, backtrack_lr=None)
+
+    global_num_off_iters = 0
+    original_lr = learning_rate
+
+    while epoch < num_epochs:
+        _sync()
+        t0 = time.time()
+        last_valid_target_policy.load_state_dict(behavioral_policy.state_dict())
+
+        states, actions, real_traj_lengths, next_states, distances, indices = \
+            collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len,
+                                              state_filter, k, num_workers)
+
+        def on_accept(num_off_iters, entropy, kl, lr):
+            nonlocal global_num_off_iters
+            global_num_off_iters += 1
+            log_off_iter_statistics(writer, csv_file_3, epoch, global_num_off_iters,
+                                    num_off_iters - 1, entropy, kl, lr)
+
+        res = off_policy_optimization(
+            optimizer, behavioral_policy, target_policy, last_valid_target_policy, states,
+            actions, num_traj, real_traj_lengths, distances, indices, k, G, B, ns, eps,
+            kl_threshold, max_off_iters, use_backtracking, backtrack_coeff, max_backtrack_try,
+            original_lr if use_backtracking else learning_rate, on_accept)
+        entropy, num_off_iters, backtrack_iter, learning_rate = res
+        if torch.isnan(entropy) or torch.isinf(entropy):
+            print("Aborting because final entropy is nan or inf...")
+            print("There is most likely a problem in knn aliasing. Use a higher k.")
+            raise SystemExit(0)
+        epoch += 1
+        behavioral_policy.load_state_dict(last_valid_target_policy.state_dict())
+        target_policy.load_state_dict(last_valid_target_policy.state_dict())
+        loss = -_np(entropy)
+        entropy = _np(entropy)
+        execution_time = time.time() - t0
+
+        if epoch % heatmap_every == 0:
+            states, actions, real_traj_lengths, next_states, distances, indices = \
+                collect_particles_and_compute_knn(env, behavioral_policy,
+                                                  num_traj * full_entropy_traj_scale, traj_len,
+                                                  state_filter, full_entropy_k, num_workers)
+            with torch.no_grad():
+                full_entropy = compute_entropy(behavioral_policy, behavioral_policy, states,
+                                               actions, num_traj * full_entropy_traj_scale,
+                                               real_traj_lengths, distances, indices,
+                                               full_entropy_k, G, full_B, ns, eps)
+            full_entropy = _np(full_entropy)
+            _save_policy(behavioral_policy, os.path.join(out_path, f"{epoch}-policy"))
+        log_epoch_statistics(writer=writer, log_file=log_file, csv_file_1=csv_file_1,
+                             csv_file_2=csv_file_2, epoch=epoch, loss=loss, entropy=entropy,
+                             execution_time=execution_time, num_off_iters=num_off_iters,
+                             full_entropy=full_entropy, heatmap_image=None, heatmap_entropy=None,
+                             backtrack_iters=backtrack_iter, backtrack_lr=learning_rate)
+    return behavioral_policy
+
+
+def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_valid_target_policy,
+                            states, actions, num_traj, real_traj_lengths, distances, indices, k, G,
+                            B, ns, eps, kl_threshold, max_off_iters, use_backtracking,
+                            backtrack_coeff, max_backtrack_try, original_lr, on_accept=None):
+    """The off-policy loop of one epoch with KL acceptance and backtracking (mepol.py:416-483).
+
+    Returns (final entropy of the last valid target as a 0-d tensor, num_off_iters,
+    backtrack_iter, learning_rate).  last_valid_target_policy must hold the behavioral
+    parameters on entry (mepol.py:409).
+    """
+    kl_threshold_reached = False
+    num_off_iters = 0
+    learning_rate = original_lr
+    if use_backtracking:
+        for param_group in optimizer.param_groups:
+            param_group["lr"] = learning_rate
+        backtrack_iter = 1
+    else:
+        backtrack_iter = None
+
+    while not kl_threshold_reached:
+        loss, numeric_error = policy_update(optimizer, behavioral_policy, target_policy, states,
+                                            actions, num_traj, real_traj_lengths, distances,
+                                            indices, k, G, B, ns, eps)
+        entropy = -_np(loss)
+        kl, kl_numeric_error = compute_kl(behavioral_policy, target_policy, states, actions,
+                                          num_traj, real_traj_lengths, distances, indices, k, eps)
+        kl = _np(kl)
+
+        if not numeric_error and not kl_numeric_error and kl <= kl_threshold:
+            last_valid_target_policy.load_state_dict(target_policy.state_dict())
+            num_off_iters += 1
+            if on_accept is not None:
+                on_accept(num_off_iters, entropy, kl, learning_rate)
+        else:
+            if use_backtracking:
+                if not backtrack_iter == max_backtrack_try:
+                    target_policy.load_state_dict(last_valid_target_policy.state_dict())
+                    learning_rate = original_lr / (backtrack_coeff ** backtrack_iter)
+                    for param_group in optimizer.param_groups:
+                        param_group["lr"] = learning_rate
+                    backtrack_iter += 1
+                    continue
+            kl_threshold_reached = True
+
+        if use_backtracking and backtrack_iter > 1:
+            kl_threshold_reached = True
+        if num_off_iters == max_off_iters:
+            kl_threshold_reached = True
+
+    with torch.no_grad():
+        entropy = compute_entropy(last_valid_target_policy, last_valid_target_policy, states,
+                                  actions, num_traj, real_traj_lengths, distances, indices, k, G,
+                                  B, ns, eps)
+    return entropy, num_off_iters, backtrack_iter, learning_rate
+
+
+def _np(x):
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy()
+    return x
+
+
+def _sync():
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()

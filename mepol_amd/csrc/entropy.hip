@@ -1,0 +1,419 @@
+// Importance weights, Kozachenko-Leonenko entropy / KL estimate and their gradient on gfx950.
+//
+// Reference (src/algorithms/mepol.py):
+//   compute_importance_weights  :114-139   u_{n,t} = exp(cumsum_t(logp_T - logp_B)), w = u / sum(u)
+//   compute_entropy             :142-154   W_i = sum_{c<k} w[I[i,c]]      (I[:, :-1]: self + k-1)
+//                                          V_i = D[i,k]^ns pi^(ns/2) / G
+//                                          H   = -sum_i (W_i/k) log(W_i/(V_i+eps) + eps) + B
+//   compute_kl                  :157-174   KL  = (1/N) sum_i log(k/(N W_i) + eps)
+//   policy_update / backward    :268-281   autograd through gather -> normalise -> exp/cumsum.
+//
+// The backward is the closed form of that autograd chain:
+//   g_i     = dH/dW_i = -(1/k) [ln(r_i + eps) + r_i/(r_i + eps)],  r_i = W_i/(V_i + eps)
+//   gamma_j = sum_{(i,c<k): I[i,c] = j} g_i               (deterministic CSR transpose of I)
+//   S       = sum_j gamma_j w_j
+//   dH/dDelta_{n,s} = sum_{t>=s} (gamma_{n,t} - S) w_{n,t}  (segmented reverse scan)
+// and is handed to torch autograd as the gradient of logp_T (the MLP backward stays in torch).
+//
+// Everything is f64 (the reference's dtype, src/utils/dtypes.py:3) and every reduction has a
+// fixed order, so results are bitwise reproducible run to run.
+//
+// Particle layout: trajectory n owns particles [off[n], off[n+1]); logp/grad arrays are dense
+// [nt, T_stride] with t < len_n = off[n+1]-off[n] (mepol.py:121-136, ragged via real lengths).
+#include "common.hpp"
+
+#include <algorithm>
+
+namespace mepol {
+namespace ent {
+
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------------------------------------
+// IW forward: one wave per trajectory, chunked inclusive scan of Delta, then exp.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void iw_scan_kernel(const double* __restrict__ logp_t,
+                                                      const double* __restrict__ logp_b,
+                                                      int64_t nt, int64_t T_stride,
+                                                      const int64_t* __restrict__ off,
+                                                      double* __restrict__ u,
+                                                      double* __restrict__ traj_sum) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t n = (int64_t)blockIdx.x * 4 + w;
+  if (n >= nt) return;
+  const int64_t p0 = off[n];
+  const int64_t len = off[n + 1] - p0;
+  const int64_t chunk = (len + 63) / 64;
+  const int64_t b = l * chunk, e = min(len, b + chunk);
+  const double* lt = logp_t + n * T_stride;
+  const double* lb = logp_b + n * T_stride;
+  // lane-local sum of its chunk
+  double s = 0.0;
+  for (int64_t t = b; t < e; ++t) s += lt[t] - lb[t];
+  // exclusive wave scan of lane sums
+  double incl = s;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    const double o = __shfl_up(incl, m, kWave);
+    if (l >= m) incl += o;
+  }
+  double run = incl - s;
+  double usum = 0.0;
+  for (int64_t t = b; t < e; ++t) {
+    run += lt[t] - lb[t];
+    const double x = exp(run);
+    u[p0 + t] = x;
+    usum += x;
+  }
+  usum = wave_sum(usum);
+  if (l == 0) traj_sum[n] = usum;
+}
+
+// Deterministic block-redundant reduction of a short array (every block gets the same value).
+__device__ double block_reduce_array(const double* __restrict__ a, int64_t n, double* sh) {
+  double s = 0.0;
+  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += a[i];
+  s = wave_sum(s);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) sh[w] = s;
+  __syncthreads();
+  double tot = 0.0;
+  const int nw = blockDim.x >> 6;
+  for (int i = 0; i < nw; ++i) tot += sh[i];
+  __syncthreads();
+  return tot;
+}
+
+__global__ __launch_bounds__(256) void iw_normalize_kernel(const double* __restrict__ u,
+                                                           const double* __restrict__ traj_sum,
+                                                           int64_t nt, int64_t N,
+                                                           double* __restrict__ w,
+                                                           double* __restrict__ Uout) {
+  __shared__ double sh[4];
+  const double U = block_reduce_array(traj_sum, nt, sh);
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < N) w[i] = u[i] / U;
+  if (i == 0 && Uout) *Uout = U;
+}
+
+// ---------------------------------------------------------------------------------------
+// Entropy / KL forward: gather W, volumes, per-particle terms, block partial sums.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void entropy_fwd_kernel(
+    const double* __restrict__ w, const int32_t* __restrict__ idxT, const double* __restrict__ D,
+    int64_t N, int64_t N_w, int k, int kp1, double ns, double pi_ns2_over_G, double eps,
+    double* __restrict__ W_out, double* __restrict__ g_out, double* __restrict__ partials) {
+  __shared__ double sh[2][4];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double th = 0.0, tk = 0.0;
+  if (i < N) {
+    double Wi = 0.0;
+    for (int c = 0; c < k; ++c) Wi += w[idxT[(int64_t)c * N + i]];
+    const double V = pow(D[i * kp1 + k], ns) * pi_ns2_over_G;
+    const double r = Wi / (V + eps);
+    const double lr = log(r + eps);
+    th = (Wi / k) * lr;
+    tk = log((double)k / ((double)N_w * Wi) + eps);
+    W_out[i] = Wi;
+    g_out[i] = -(1.0 / k) * (lr + r / (r + eps));
+  }
+  th = wave_sum(th);
+  tk = wave_sum(tk);
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) {
+    sh[0][wv] = th;
+    sh[1][wv] = tk;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x + 0] = sh[0][0] + sh[0][1] + sh[0][2] + sh[0][3];
+    partials[2 * blockIdx.x + 1] = sh[1][0] + sh[1][1] + sh[1][2] + sh[1][3];
+  }
+}
+
+// out[0] = H = -sum(term) + B ; out[1] = KL (unclamped) = sum(kl_term)/N_w ;
+// out[2] = sum(term) ; out[3] = sum(kl_term)  (raw sums for multi-rank reduction)
+__global__ __launch_bounds__(256) void entropy_finalize_kernel(const double* __restrict__ partials,
+                                                               int64_t nblocks, double B,
+                                                               int64_t N_w,
+                                                               double* __restrict__ out) {
+  __shared__ double sh[4];
+  double a = 0.0, b = 0.0;
+  for (int64_t i = threadIdx.x; i < nblocks; i += blockDim.x) {
+    a += partials[2 * i];
+    b += partials[2 * i + 1];
+  }
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __shared__ double sb[4];
+  if (l == 0) {
+    sh[wv] = a;
+    sb[wv] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double ta = sh[0] + sh[1] + sh[2] + sh[3];
+    const double tb = sb[0] + sb[1] + sb[2] + sb[3];
+    out[0] = -ta + B;
+    out[1] = (1.0 / (double)N_w) * tb;
+    out[2] = ta;
+    out[3] = tb;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// CSR transpose of I[:, :k] (built once per epoch: indices are fixed within an epoch).
+// ---------------------------------------------------------------------------------------
+// Candidate ids j are global; this CSR covers the owned range [col_offset, col_offset+ncand).
+__global__ void csr_count_kernel(const int32_t* __restrict__ idxT, int64_t nq, int k,
+                                 int64_t col_offset, int64_t ncand, int32_t* __restrict__ count) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nq * (int64_t)k) return;
+  const int64_t j = (int64_t)idxT[e] - col_offset;  // idxT is [>=k][nq]: first k rows contiguous
+  if (j >= 0 && j < ncand) atomicAdd(&count[j], 1);
+}
+
+// Single-block exclusive scan of count[0..n) into off[0..n] (off[n] = total).
+__global__ __launch_bounds__(1024) void scan_kernel(const int32_t* __restrict__ count, int64_t n,
+                                                    int32_t* __restrict__ off) {
+  __shared__ int64_t sh[1024];
+  const int tid = threadIdx.x;
+  const int64_t chunk = (n + 1023) / 1024;
+  const int64_t b = tid * chunk, e = min(n, b + chunk);
+  int64_t s = 0;
+  for (int64_t i = b; i < e; ++i) s += count[i];
+  sh[tid] = s;
+  __syncthreads();
+  for (int m = 1; m < 1024; m <<= 1) {
+    int64_t v = (tid >= m) ? sh[tid - m] : 0;
+    __syncthreads();
+    sh[tid] += v;
+    __syncthreads();
+  }
+  int64_t run = sh[tid] - s;
+  for (int64_t i = b; i < e; ++i) {
+    off[i] = (int32_t)run;
+    run += count[i];
+  }
+  if (tid == 1023) off[n] = (int32_t)sh[1023];
+}
+
+__global__ void csr_fill_kernel(const int32_t* __restrict__ idxT, int64_t nq, int k,
+                                int64_t col_offset, int64_t ncand, int64_t row_offset,
+                                const int32_t* __restrict__ off, int32_t* __restrict__ cursor,
+                                int32_t* __restrict__ rows) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nq * (int64_t)k) return;
+  const int64_t j = (int64_t)idxT[e] - col_offset;
+  if (j < 0 || j >= ncand) return;
+  const int64_t i = e % nq;
+  const int32_t pos = off[j] + atomicAdd(&cursor[j], 1);
+  rows[pos] = (int32_t)(i + row_offset);
+}
+
+// Sort each segment ascending so gamma sums in a fixed order (bitwise-reproducible).
+__global__ void csr_sort_kernel(const int32_t* __restrict__ off, int64_t n, int32_t* __restrict__ rows) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int32_t b = off[j], e = off[j + 1];
+  for (int32_t x = b + 1; x < e; ++x) {
+    const int32_t v = rows[x];
+    int32_t y = x - 1;
+    while (y >= b && rows[y] > v) {
+      rows[y + 1] = rows[y];
+      --y;
+    }
+    rows[y + 1] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Backward.
+// ---------------------------------------------------------------------------------------
+// gamma_j = sum over CSR segment of g_i ; block partials of sum_j gamma_j w_j.
+__global__ __launch_bounds__(256) void gamma_kernel(const double* __restrict__ g,
+                                                    const double* __restrict__ w,
+                                                    const int32_t* __restrict__ off,
+                                                    const int32_t* __restrict__ rows, int64_t n,
+                                                    double* __restrict__ gamma,
+                                                    double* __restrict__ partials) {
+  __shared__ double sh[4];
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  double s = 0.0;
+  if (j < n) {
+    double gj = 0.0;
+    const int32_t b = off[j], e = off[j + 1];
+    for (int32_t x = b; x < e; ++x) gj += g[rows[x]];
+    gamma[j] = gj;
+    s = gj * w[j];
+  }
+  s = wave_sum(s);
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) sh[wv] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partials[blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
+}
+
+// grad_logp[n, s] = gH * sum_{t >= s} (gamma_{n,t} - S) w_{n,t} ; S = sum(partials) (or *S_ext).
+__global__ __launch_bounds__(256) void reverse_scan_kernel(
+    const double* __restrict__ gamma, const double* __restrict__ w,
+    const double* __restrict__ partials, int64_t nparts, const double* __restrict__ S_ext,
+    const int64_t* __restrict__ off, int64_t nt, int64_t T_stride,
+    const double* __restrict__ gH, double* __restrict__ grad_logp) {
+  __shared__ double sh[4];
+  const double S = S_ext ? *S_ext : block_reduce_array(partials, nparts, sh);
+  const double up = *gH;
+  const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
+  const int64_t n = (int64_t)blockIdx.x * 4 + wv;
+  if (n >= nt) return;
+  const int64_t p0 = off[n];
+  const int64_t len = off[n + 1] - p0;
+  const int64_t chunk = (len + 63) / 64;
+  const int64_t b = l * chunk, e = min(len, b + chunk);
+  double s = 0.0;
+  for (int64_t t = e - 1; t >= b; --t) s += (gamma[p0 + t] - S) * w[p0 + t];
+  // exclusive suffix scan over lanes (lanes above contribute)
+  double incl = s;
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) {
+    const double o = __shfl_down(incl, m, kWave);
+    if (l + m < 64) incl += o;
+  }
+  double run = incl - s;
+  double* gout = grad_logp + n * T_stride;
+  for (int64_t t = e - 1; t >= b; --t) {
+    run += (gamma[p0 + t] - S) * w[p0 + t];
+    gout[t] = up * run;
+  }
+  // zero the padded tail of a ragged trajectory
+  for (int64_t t = len + l; t < T_stride; t += 64) gout[t] = 0.0;
+}
+
+}  // namespace ent
+}  // namespace mepol
+
+using namespace mepol;
+using namespace mepol::ent;
+
+extern "C" int mepol_iw_forward(const double* logp_t, const double* logp_b, int64_t num_traj,
+                                int64_t T_stride, const int64_t* traj_offsets, int64_t n_particles,
+                                double* u_out, double* traj_sum_out, double* w_out, double* U_out,
+                                void* stream) {
+  if (num_traj <= 0 || T_stride <= 0 || !logp_t || !logp_b || !traj_offsets || !u_out ||
+      !traj_sum_out) {
+    set_error("mepol_iw_forward: bad arguments");
+    return kErrBadArg;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(iw_scan_kernel, dim3((unsigned)((num_traj + 3) / 4)), dim3(256), 0, st, logp_t,
+                     logp_b, num_traj, T_stride, traj_offsets, u_out, traj_sum_out);
+  MEPOL_CHECK_LAUNCH();
+  if (w_out) {
+    hipLaunchKernelGGL(iw_normalize_kernel, dim3((unsigned)((n_particles + 255) / 256)), dim3(256), 0,
+                       st, u_out, traj_sum_out, num_traj, n_particles, w_out, U_out);
+    MEPOL_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+// Normalise u by an externally supplied total (multi-rank: U = all-reduce of local sums).
+__global__ void scale_by_kernel(const double* __restrict__ u, const double* __restrict__ U,
+                                int64_t n, double* __restrict__ w) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) w[i] = u[i] / *U;
+}
+
+extern "C" int mepol_iw_normalize(const double* u, const double* U, int64_t n, double* w,
+                                  void* stream) {
+  hipLaunchKernelGGL(scale_by_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, u, U, n, w);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mepol_entropy_partials_size(int64_t n_particles) {
+  return (int)((n_particles + kBlock - 1) / kBlock);
+}
+
+// w: [N_w] (all particles, global indexing); idxT: [kp1][n] transposed neighbour indices of the
+// n local query particles; D: [n][kp1].  out4 = {H, KL_unclamped, sum term, sum kl_term}.
+extern "C" int mepol_entropy_forward(const double* w, const int32_t* idxT, const double* D,
+                                     int64_t n, int64_t n_w, int k, int kp1, double ns, double G,
+                                     double B, double eps, double* W_out, double* g_out,
+                                     double* partials, double* out4, void* stream) {
+  if (n < 0 || k <= 0 || kp1 <= k || !w || !idxT || !D || !W_out || !g_out || !partials || !out4) {
+    set_error("mepol_entropy_forward: bad arguments");
+    return kErrBadArg;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t nb = (n + kBlock - 1) / kBlock;
+  const double pi_ns2_over_G = pow(M_PI, ns / 2.0) / G;
+  if (nb > 0) {
+    hipLaunchKernelGGL(entropy_fwd_kernel, dim3((unsigned)nb), dim3(kBlock), 0, st, w, idxT, D, n,
+                       n_w, k, kp1, ns, pi_ns2_over_G, eps, W_out, g_out, partials);
+    MEPOL_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(entropy_finalize_kernel, dim3(1), dim3(256), 0, st, partials, nb, B, n_w, out4);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}
+
+// CSR transpose of the first k rows of idxT ([>=k][nq]): for every owned candidate id
+// j in [col_offset, col_offset + ncand) the sorted list of query rows (row_offset + i) whose
+// first k neighbours contain j.  csr_off: [ncand+1]; csr_rows: [nq*k]; scratch: [ncand] int32.
+extern "C" int mepol_csr_build(const int32_t* idxT, int64_t nq, int k, int64_t col_offset,
+                               int64_t ncand, int64_t row_offset, int32_t* csr_off,
+                               int32_t* csr_rows, int32_t* scratch, void* stream) {
+  if (!idxT || !csr_off || !csr_rows || !scratch || k <= 0 || ncand <= 0) {
+    set_error("mepol_csr_build: bad arguments");
+    return kErrBadArg;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t ne = nq * (int64_t)k;
+  MEPOL_HIP(hipMemsetAsync(scratch, 0, ncand * sizeof(int32_t), st));
+  if (ne > 0) {
+    hipLaunchKernelGGL(csr_count_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, idxT,
+                       nq, k, col_offset, ncand, scratch);
+    MEPOL_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, scratch, ncand, csr_off);
+  MEPOL_CHECK_LAUNCH();
+  MEPOL_HIP(hipMemsetAsync(scratch, 0, ncand * sizeof(int32_t), st));
+  if (ne > 0) {
+    hipLaunchKernelGGL(csr_fill_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, idxT,
+                       nq, k, col_offset, ncand, row_offset, csr_off, scratch, csr_rows);
+    MEPOL_CHECK_LAUNCH();
+  }
+  hipLaunchKernelGGL(csr_sort_kernel, dim3((unsigned)((ncand + 255) / 256)), dim3(256), 0, st,
+                     csr_off, ncand, csr_rows);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}
+
+// gamma over the n_own particles this rank owns (CSR over its own ids), partial S per block.
+extern "C" int mepol_entropy_gamma(const double* g, const double* w_own, const int32_t* csr_off,
+                                   const int32_t* csr_rows, int64_t n_own, double* gamma_out,
+                                   double* partials, void* stream) {
+  const int64_t nb = (n_own + 255) / 256;
+  if (nb == 0) return 0;
+  hipLaunchKernelGGL(gamma_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, g, w_own,
+                     csr_off, csr_rows, n_own, gamma_out, partials);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}
+
+// grad_logp [nt, T_stride] from gamma / w of the local trajectories.  S is either reduced from
+// `partials` (nparts of them, single-rank) or read from S_ext (multi-rank all-reduced value).
+extern "C" int mepol_entropy_reverse_scan(const double* gamma, const double* w,
+                                          const double* partials, int64_t nparts,
+                                          const double* S_ext, const int64_t* traj_offsets,
+                                          int64_t num_traj, int64_t T_stride, const double* grad_H,
+                                          double* grad_logp, void* stream) {
+  if (num_traj <= 0) return 0;
+  hipLaunchKernelGGL(reverse_scan_kernel, dim3((unsigned)((num_traj + 3) / 4)), dim3(256), 0,
+                     (hipStream_t)stream, gamma, w, partials, nparts, S_ext, traj_offsets, num_traj,
+                     T_stride, grad_H, grad_logp);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,714 @@
+// All-pairs exact k-NN for the MEPOL particle batch on gfx950 (CDNA4, wave64).
+//
+// Replaces the sklearn call of the reference
+//   nbrs = NearestNeighbors(n_neighbors=k+1, metric='euclidean', algorithm='auto')
+//   nbrs.fit(next_states); distances, indices = nbrs.kneighbors(next_states)
+// (src/algorithms/mepol.py:190-192).  Output contract = the pinned sklearn 0.22 kd_tree:
+// distances are sqrt(sum_f (x_f - y_f)^2) evaluated in f64 over the f32 inputs, rows sorted
+// ascending; ties are broken by the smaller candidate index (sklearn leaves tie order
+// implementation-defined, so this is the build's documented convention).
+//
+// Pipeline (all on one stream, no host sync, no allocation):
+//   1. pack    : candidates -> MFMA A-fragment tiles, A = [-2 c, |c|^2] (fp32), max |c|.
+//   2. select  : v_mfma_f32_32x32x2_f32 computes |c|^2 - 2 q.c for 32 candidates x 32 queries
+//                per 15-MFMA step (d = 29); each lane owns one query column and keeps a
+//                sorted top-LIST list in VGPRs, fed through a per-lane LDS buffer so the
+//                wave pays the insertion cost in batches, not per candidate.
+//   3. refine  : per query, merge the 2*split partial lists to the approximate top-LIST,
+//                recompute those distances exactly in f64, bitonic-sort by (dist, idx), and
+//                certify with a rigorous fp32 error bound that no excluded candidate can
+//                enter the top-(k+1).  Uncertified queries (near-ties across the boundary,
+//                large duplicate clusters) are queued.
+//   4. exact   : queued queries are answered by an exhaustive f64 scan (no approximation).
+#include "common.hpp"
+
+#include <algorithm>
+#include <cfloat>
+#include <climits>
+
+namespace mepol {
+namespace knn {
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+constexpr float kPadNorm = 1e30f;  // |c|^2 of padding candidates: never selected
+constexpr int kBufCap = 24;        // per-lane LDS insertion buffer (entries)
+constexpr int kMaxSplit = 16;
+
+// ---------------------------------------------------------------------------------------
+// 1. pack
+// ---------------------------------------------------------------------------------------
+// apack[(t*64 + l)*KSP + s] = A[i = l&31][k = l>>5] of k-step s for candidate tile t, i.e.
+// feature f = 2s + (l>>5) of candidate c = 32t + (l&31):  f<d: -2 x_cf ; f==d: |c|^2 ; else 0.
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                   int KSP, int64_t nct,
+                                                   float* __restrict__ apack,
+                                                   unsigned* __restrict__ cmax_bits) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = nct * 64;
+  float mynorm = 0.f;
+  if (gid < total) {
+    const int64_t t = gid >> 6;
+    const int l = (int)(gid & 63);
+    const int h = l >> 5;
+    const int64_t c = t * 32 + (l & 31);
+    const bool valid = c < n;
+    float cn = 0.f;
+    if (valid) {
+      const float* xc = X + c * d;
+      for (int f = 0; f < d; ++f) cn = fmaf(xc[f], xc[f], cn);
+    }
+    float* dst = apack + gid * KSP;
+    for (int s = 0; s < KSP; s += 4) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int f = 2 * (s + u) + h;
+        float x;
+        if (valid)
+          x = (f < d) ? -2.f * X[c * d + f] : ((f == d) ? cn : 0.f);
+        else
+          x = (f == d) ? kPadNorm : 0.f;
+        v[u] = x;
+      }
+      *reinterpret_cast<float4*>(dst + s) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    if (valid && h == 0) mynorm = sqrtf(cn);
+  }
+  // wave max -> one atomic per wave (non-negative floats order like their bit patterns)
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) mynorm = fmaxf(mynorm, __shfl_xor(mynorm, m, kWave));
+  if ((threadIdx.x & 63) == 0) atomicMax(cmax_bits, __float_as_uint(mynorm));
+}
+
+// ---------------------------------------------------------------------------------------
+// 2. select
+// ---------------------------------------------------------------------------------------
+template <int LIST>
+__device__ __forceinline__ void list_insert(float (&ld)[LIST], int (&li)[LIST], float x, int xi) {
+  // ld ascending; precondition x < ld[LIST-1].  Branch-free shift-insert.
+  bool c[LIST];
+#pragma unroll
+  for (int j = 0; j < LIST; ++j) c[j] = x < ld[j];
+#pragma unroll
+  for (int j = LIST - 1; j >= 1; --j) {
+    ld[j] = c[j - 1] ? ld[j - 1] : (c[j] ? x : ld[j]);
+    li[j] = c[j - 1] ? li[j - 1] : (c[j] ? xi : li[j]);
+  }
+  ld[0] = c[0] ? x : ld[0];
+  li[0] = c[0] ? xi : li[0];
+}
+
+// Merge this lane's LDS buffer into its sorted list; then share the prune bound with the
+// partner lane (l ^ 32 serves the same query column).  Every lane of the wave calls it.
+template <int LIST>
+__device__ __forceinline__ void flush_buffer(float (&ld)[LIST], int (&li)[LIST], float& thr, int& cnt,
+                                             const float (*bv)[64], const int (*bi)[64], int l) {
+  const int mc = wave_max_i(cnt);
+#pragma nounroll
+  for (int e = 0; e < mc; ++e) {
+    if (e < cnt) {
+      const float x = bv[e][l];
+      const int xi = bi[e][l];
+      if (x < thr) {
+        list_insert<LIST>(ld, li, x, xi);
+        thr = ld[LIST - 1];
+      }
+    }
+  }
+  cnt = 0;
+  // lanes l and l^32 serve the same query: the tighter of their maxima is a valid prune bound
+  // for both (refine's certification bound is the min over all partial-list maxima).
+  thr = fminf(ld[LIST - 1], __shfl_xor(ld[LIST - 1], 32, kWave));
+}
+
+// Row (candidate within the tile) of accumulator register r for lane l (32x32 C/D map).
+__device__ __forceinline__ int acc_row(int r, int l) { return (r & 3) + 8 * (r >> 2) + 4 * (l >> 5); }
+
+template <int KS, int KSP, int LIST>
+__global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ apack,
+                                                     const float* __restrict__ query, int64_t nq,
+                                                     int d, int64_t nct, int split,
+                                                     int64_t tiles_per_split,
+                                                     float* __restrict__ out_v,
+                                                     int* __restrict__ out_i) {
+  __shared__ float sbuf_v[4][kBufCap][64];
+  __shared__ int sbuf_i[4][kBufCap][64];
+  const int w = threadIdx.x >> 6;
+  const int l = threadIdx.x & 63;
+  const int64_t qt = (int64_t)blockIdx.x * 4 + w;
+  const int sp = blockIdx.y;
+  if (qt * 32 >= nq) return;  // wave-uniform
+  const int h = l >> 5;
+  const int64_t q = qt * 32 + (l & 31);
+  const bool qvalid = q < nq;
+
+  // B operand (queries): B[k = h][j = l&31] of step s = feature 2s + h; f == d carries 1.
+  float bq[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int f = 2 * s + h;
+    bq[s] = qvalid ? ((f < d) ? query[q * d + f] : ((f == d) ? 1.f : 0.f)) : 0.f;
+  }
+
+  float ld[LIST];
+  int li[LIST];
+#pragma unroll
+  for (int j = 0; j < LIST; ++j) {
+    ld[j] = INFINITY;
+    li[j] = -1;
+  }
+  float thr = INFINITY;
+  int cnt = 0;
+
+  const int64_t t0 = (int64_t)sp * tiles_per_split;
+  const int64_t t1 = min(nct, t0 + tiles_per_split);
+
+  constexpr int NV = KSP / 4;
+  float an[KSP];
+  const float* abase = apack + (int64_t)l * KSP;
+  auto load_tile = [&](int64_t t) {
+    const float4* p = reinterpret_cast<const float4*>(abase + t * 64 * KSP);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const float4 x = p[v];
+      an[4 * v + 0] = x.x;
+      an[4 * v + 1] = x.y;
+      an[4 * v + 2] = x.z;
+      an[4 * v + 3] = x.w;
+    }
+  };
+  if (t0 < t1) load_tile(t0);
+
+#pragma nounroll
+  for (int64_t t = t0; t < t1; ++t) {
+    float a[KSP];
+#pragma unroll
+    for (int v = 0; v < KSP; ++v) a[v] = an[v];
+    if (t + 1 < t1) load_tile(t + 1);
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bq[s], acc, 0, 0, 0);
+
+    float m = fminf(fminf(fminf(acc[0], acc[1]), fminf(acc[2], acc[3])),
+                    fminf(fminf(acc[4], acc[5]), fminf(acc[6], acc[7])));
+    m = fminf(m, fminf(fminf(fminf(acc[8], acc[9]), fminf(acc[10], acc[11])),
+                       fminf(fminf(acc[12], acc[13]), fminf(acc[14], acc[15]))));
+    if (__ballot(m < thr)) {
+      const int base = (int)(t * 32);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (acc[r] < thr) {
+          sbuf_v[w][cnt][l] = acc[r];
+          sbuf_i[w][cnt][l] = base + acc_row(r, l);
+          ++cnt;
+        }
+      }
+      if (__ballot(cnt > kBufCap - 16)) flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l);
+    }
+  }
+  flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l);
+
+  if (qvalid) {
+    const int64_t o = ((q * split + sp) * 2 + h) * LIST;
+#pragma unroll
+    for (int j = 0; j < LIST; ++j) {
+      out_v[o + j] = ld[j];
+      out_i[o + j] = li[j];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// 3. refine + certify
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ bool lex_less(double a, int ai, double b, int bi) {
+  return a < b || (a == b && ai < bi);
+}
+__device__ __forceinline__ bool lex_less_f(float a, int ai, float b, int bi) {
+  return a < b || (a == b && ai < bi);
+}
+
+// Exact f64 squared distance, summed in feature order with no contraction (matches the
+// reference's kd_tree rdist: sum of (x_f - y_f)^2 in double, f = 0..d-1).
+__device__ __forceinline__ double exact_d2(const float* __restrict__ a, const float* __restrict__ b, int d) {
+  double s = 0.0;
+  for (int f = 0; f < d; ++f) {
+    const double t = __dsub_rn((double)a[f], (double)b[f]);
+    s = __dadd_rn(s, __dmul_rn(t, t));
+  }
+  return s;
+}
+
+template <int LIST, int MAXP>
+__global__ __launch_bounds__(256) void refine_kernel(
+    const float* __restrict__ cand, int64_t nc, const float* __restrict__ query, int64_t nq, int d,
+    int kp1, int split, const float* __restrict__ lists_v, const int* __restrict__ lists_i,
+    const unsigned* __restrict__ cmax_bits, double* __restrict__ Dout, int64_t* __restrict__ I64,
+    int32_t* __restrict__ I32, int* __restrict__ flag_count, int* __restrict__ flag_list) {
+  __shared__ int sel[4][64];
+  const int w = threadIdx.x >> 6;
+  const int l = threadIdx.x & 63;
+  const int64_t q = (int64_t)blockIdx.x * 4 + w;
+  if (q >= nq) return;
+  const int M = 2 * split * LIST;
+  const float* lv = lists_v + q * M;
+  const int* lix = lists_i + q * M;
+
+  // Bound part 1: min over partial lists of their maxima (last, lists are ascending).
+  float bnd = INFINITY;
+  for (int p = l; p < 2 * split; p += 64) bnd = fminf(bnd, lv[p * LIST + LIST - 1]);
+
+  float ev[MAXP];
+  int ei[MAXP];
+#pragma unroll
+  for (int p = 0; p < MAXP; ++p) {
+    const int e = p * 64 + l;
+    float v = INFINITY;
+    int ix = INT_MAX;
+    if (e < M) {
+      const int ii = lix[e];
+      if (ii >= 0 && ii < nc) {
+        v = lv[e];
+        ix = ii;
+      }
+    }
+    ev[p] = v;
+    ei[p] = ix;
+  }
+  // LIST rounds of wave argmin over (approx, idx): approximate top-LIST of the union.
+  float last = INFINITY;
+#pragma nounroll
+  for (int r = 0; r < LIST; ++r) {
+    float bv = ev[0];
+    int bi = ei[0];
+#pragma unroll
+    for (int p = 1; p < MAXP; ++p)
+      if (lex_less_f(ev[p], ei[p], bv, bi)) {
+        bv = ev[p];
+        bi = ei[p];
+      }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      const float ov = __shfl_xor(bv, m, kWave);
+      const int oi = __shfl_xor(bi, m, kWave);
+      if (lex_less_f(ov, oi, bv, bi)) {
+        bv = ov;
+        bi = oi;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p)
+      if (ei[p] == bi) ev[p] = INFINITY, ei[p] = INT_MAX;
+    if (l == 0) sel[w][r] = (bi == INT_MAX) ? -1 : bi;
+    last = bv;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) bnd = fminf(bnd, __shfl_xor(bnd, m, kWave));
+  bnd = fminf(bnd, last);
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+
+  // Exact f64 distances for the selected candidates, one per lane.
+  const float* xq = query + q * d;
+  double dd = INFINITY;
+  int di = INT_MAX;
+  if (l < LIST) {
+    const int c = sel[w][l];
+    if (c >= 0) {
+      dd = exact_d2(xq, cand + (int64_t)c * d, d);
+      di = c;
+    }
+  }
+  // Bitonic sort of 64 (dd, di) pairs across the wave, ascending.
+#pragma unroll
+  for (int size = 2; size <= 64; size <<= 1) {
+#pragma unroll
+    for (int stride = size >> 1; stride >= 1; stride >>= 1) {
+      const double od = __shfl_xor(dd, stride, kWave);
+      const int oi = __shfl_xor(di, stride, kWave);
+      const bool up = ((l & size) == 0);
+      const bool lower = ((l & stride) == 0);
+      const bool other_less = lex_less(od, oi, dd, di);
+      // lower lane keeps the min if ascending block, max otherwise
+      const bool take = (lower == up) ? other_less : !other_less && !(od == dd && oi == di);
+      if (take) {
+        dd = od;
+        di = oi;
+      }
+    }
+  }
+  // Certification: every candidate outside `sel` has exact d^2 >= bnd + |q|^2 - E.
+  double qn2 = 0.0;
+  for (int f = 0; f < d; ++f) qn2 += (double)xq[f] * (double)xq[f];
+  const double cmax = (double)__uint_as_float(*cmax_bits);
+  const double E = 4.0 * (double)(d + 1) * 5.9604644775390625e-08 * (cmax * cmax + cmax * sqrt(qn2)) +
+                   1e-300;
+  const double ek = __shfl(dd, kp1 - 1, kWave);
+  const int eki = __shfl(di, kp1 - 1, kWave);
+  bool ok = (eki != INT_MAX);
+  if (bnd < 1e29f) ok = ok && (ek < ((double)bnd + qn2) - E);
+  if (l < kp1) {
+    Dout[q * kp1 + l] = sqrt(dd);
+    if (I64) I64[q * kp1 + l] = di;
+    if (I32) I32[q * kp1 + l] = di;
+  }
+  if (!ok && l == 0) {
+    const int slot = atomicAdd(flag_count, 1);
+    flag_list[slot] = (int)q;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// 4. exhaustive exact fallback for uncertified queries
+// ---------------------------------------------------------------------------------------
+template <int LIST>
+__global__ __launch_bounds__(256) void exact_kernel(const float* __restrict__ cand, int64_t nc,
+                                                    const float* __restrict__ query, int d, int kp1,
+                                                    const int* __restrict__ flag_count,
+                                                    const int* __restrict__ flag_list,
+                                                    double* __restrict__ Dout,
+                                                    int64_t* __restrict__ I64,
+                                                    int32_t* __restrict__ I32) {
+  __shared__ double red_d[4];
+  __shared__ int red_i[4];
+  const int tid = threadIdx.x;
+  const int l = tid & 63, w = tid >> 6;
+  const int count = *flag_count;
+  for (int fi = blockIdx.x; fi < count; fi += gridDim.x) {
+    const int64_t q = flag_list[fi];
+    const float* xq = query + q * d;
+    double ld[LIST];
+    int li[LIST];
+#pragma unroll
+    for (int j = 0; j < LIST; ++j) {
+      ld[j] = INFINITY;
+      li[j] = INT_MAX;
+    }
+#pragma nounroll
+    for (int64_t c = tid; c < nc; c += blockDim.x) {
+      const double x = exact_d2(xq, cand + c * d, d);
+      const int xi = (int)c;
+      if (lex_less(x, xi, ld[LIST - 1], li[LIST - 1])) {
+        bool cc[LIST];
+#pragma unroll
+        for (int j = 0; j < LIST; ++j) cc[j] = lex_less(x, xi, ld[j], li[j]);
+#pragma unroll
+        for (int j = LIST - 1; j >= 1; --j) {
+          ld[j] = cc[j - 1] ? ld[j - 1] : (cc[j] ? x : ld[j]);
+          li[j] = cc[j - 1] ? li[j - 1] : (cc[j] ? xi : li[j]);
+        }
+        ld[0] = cc[0] ? x : ld[0];
+        li[0] = cc[0] ? xi : li[0];
+      }
+    }
+    // kp1 rounds of block argmin over list heads; the winner pops its head.
+#pragma nounroll
+    for (int r = 0; r < kp1; ++r) {
+      double bd = ld[0];
+      int bi = li[0];
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) {
+        const double od = __shfl_xor(bd, m, kWave);
+        const int oi = __shfl_xor(bi, m, kWave);
+        if (lex_less(od, oi, bd, bi)) {
+          bd = od;
+          bi = oi;
+        }
+      }
+      if (l == 0) {
+        red_d[w] = bd;
+        red_i[w] = bi;
+      }
+      __syncthreads();
+      bd = red_d[0];
+      bi = red_i[0];
+#pragma unroll
+      for (int u = 1; u < 4; ++u)
+        if (lex_less(red_d[u], red_i[u], bd, bi)) {
+          bd = red_d[u];
+          bi = red_i[u];
+        }
+      __syncthreads();
+      if (li[0] == bi) {
+#pragma unroll
+        for (int j = 0; j < LIST - 1; ++j) {
+          ld[j] = ld[j + 1];
+          li[j] = li[j + 1];
+        }
+        ld[LIST - 1] = INFINITY;
+        li[LIST - 1] = INT_MAX;
+      }
+      if (tid == 0) {
+        Dout[q * kp1 + r] = sqrt(bd);
+        if (I64) I64[q * kp1 + r] = bi;
+        if (I32) I32[q * kp1 + r] = bi;
+      }
+    }
+  }
+}
+
+__global__ void fill_identity_kernel(int* s, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) s[0] = (int)n;
+  if (i < n) s[1 + i] = (int)i;
+}
+
+// ---------------------------------------------------------------------------------------
+// host-side plan + dispatch
+// ---------------------------------------------------------------------------------------
+struct Plan {
+  int d, kp1, KS, KSP, LIST, split, maxp;
+  int64_t nc, nq, nct, nqt, tiles_per_split;
+  size_t off_apack, off_scalars, off_lv, off_li, off_flag, total;
+};
+
+static const int kKSChoices[] = {2, 4, 8, 12, 15, 16, 24, 32};
+static const int kListChoices[] = {8, 16, 40, 64};
+
+static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Plan* P) {
+  if (nc <= 0 || nq < 0 || d <= 0 || kp1 <= 0) {
+    set_error("mepol_knn: bad sizes nc=%lld nq=%lld d=%d kp1=%d", (long long)nc, (long long)nq, d,
+              kp1);
+    return kErrBadArg;
+  }
+  if (kp1 > nc) {
+    set_error("mepol_knn: n_neighbors=%d > n_samples=%lld (sklearn raises the same)", kp1,
+              (long long)nc);
+    return kErrBadArg;
+  }
+  if (nc > INT_MAX - 64) {
+    set_error("mepol_knn: n_cand=%lld exceeds int32 indexing", (long long)nc);
+    return kErrUnsupported;
+  }
+  const int need_ks = (d + 1 + 1) / 2;
+  int KS = -1;
+  for (int v : kKSChoices)
+    if (v >= need_ks) {
+      KS = v;
+      break;
+    }
+  int LIST = -1;
+  for (int v : kListChoices)
+    if (v >= kp1 + 4 || (v == 64 && kp1 <= 60)) {
+      LIST = v;
+      break;
+    }
+  if (KS < 0 || LIST < 0) {
+    set_error("mepol_knn: unsupported d=%d / k+1=%d (fast path supports d<=63, k+1<=60)", d, kp1);
+    return kErrUnsupported;
+  }
+  P->d = d;
+  P->kp1 = kp1;
+  P->KS = KS;
+  P->KSP = (KS + 3) / 4 * 4;
+  P->LIST = LIST;
+  P->nc = nc;
+  P->nq = nq;
+  P->nct = (nc + 31) / 32;
+  P->nqt = (nq + 31) / 32;
+  int split = split_hint;
+  if (split <= 0) {
+    // enough waves to fill 256 CUs x ~3 waves/SIMD several times over, tiles >= 16 per split
+    const int64_t target = 16384;
+    split = (int)std::min<int64_t>(kMaxSplit, std::max<int64_t>(1, (target + P->nqt - 1) / std::max<int64_t>(P->nqt, 1)));
+    while (split > 1 && P->nct / split < 16) --split;
+  }
+  split = std::max(1, std::min(split, kMaxSplit));
+  P->split = split;
+  P->tiles_per_split = (P->nct + split - 1) / split;
+  P->maxp = (2 * split * LIST + 63) / 64;
+  size_t off = 0;
+  P->off_apack = off;
+  off = align_up(off + (size_t)P->nct * 64 * P->KSP * sizeof(float), 256);
+  P->off_scalars = off;
+  off = align_up(off + 16, 256);
+  const size_t nl = (size_t)std::max<int64_t>(nq, 1) * 2 * split * LIST;
+  P->off_lv = off;
+  off = align_up(off + nl * sizeof(float), 256);
+  P->off_li = off;
+  off = align_up(off + nl * sizeof(int), 256);
+  P->off_flag = off;
+  off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(int), 256);
+  P->total = off;
+  return 0;
+}
+
+template <int KS>
+static void launch_select_ks(const Plan& P, dim3 g, const float* ap, const float* query, float* lv,
+                             int* li, hipStream_t st) {
+  constexpr int KSP = (KS + 3) / 4 * 4;
+  switch (P.LIST) {
+    case 8:
+      hipLaunchKernelGGL((select_kernel<KS, KSP, 8>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
+                         P.nct, P.split, P.tiles_per_split, lv, li);
+      break;
+    case 16:
+      hipLaunchKernelGGL((select_kernel<KS, KSP, 16>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
+                         P.nct, P.split, P.tiles_per_split, lv, li);
+      break;
+    case 40:
+      hipLaunchKernelGGL((select_kernel<KS, KSP, 40>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
+                         P.nct, P.split, P.tiles_per_split, lv, li);
+      break;
+    default:
+      hipLaunchKernelGGL((select_kernel<KS, KSP, 64>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
+                         P.nct, P.split, P.tiles_per_split, lv, li);
+      break;
+  }
+}
+
+template <int LIST>
+static void launch_refine_list(const Plan& P, const float* cand, const float* query,
+                               const float* lv, const int* li, const unsigned* cmax, double* D,
+                               int64_t* I64, int32_t* I32, int* fc, int* fl, hipStream_t st) {
+  dim3 g((unsigned)((P.nq + 3) / 4));
+  // MAXP = ceil(2 * split * LIST / 64) for split <= kMaxSplit
+  if (P.maxp <= 2)
+    hipLaunchKernelGGL((refine_kernel<LIST, 2>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
+                       P.kp1, P.split, lv, li, cmax, D, I64, I32, fc, fl);
+  else if (P.maxp <= 4)
+    hipLaunchKernelGGL((refine_kernel<LIST, 4>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
+                       P.kp1, P.split, lv, li, cmax, D, I64, I32, fc, fl);
+  else if (P.maxp <= 8)
+    hipLaunchKernelGGL((refine_kernel<LIST, 8>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
+                       P.kp1, P.split, lv, li, cmax, D, I64, I32, fc, fl);
+  else if (P.maxp <= 16)
+    hipLaunchKernelGGL((refine_kernel<LIST, 16>), g, dim3(256), 0, st, cand, P.nc, query, P.nq,
+                       P.d, P.kp1, P.split, lv, li, cmax, D, I64, I32, fc, fl);
+  else
+    hipLaunchKernelGGL((refine_kernel<LIST, 32>), g, dim3(256), 0, st, cand, P.nc, query, P.nq,
+                       P.d, P.kp1, P.split, lv, li, cmax, D, I64, I32, fc, fl);
+}
+
+template <int LIST>
+static void launch_exact_list(const Plan& P, const float* cand, const float* query, const int* fc,
+                              const int* fl, double* D, int64_t* I64, int32_t* I32,
+                              unsigned grid, hipStream_t st) {
+  hipLaunchKernelGGL((exact_kernel<LIST>), dim3(grid), dim3(256), 0, st, cand, P.nc, query, P.d,
+                     P.kp1, fc, fl, D, I64, I32);
+}
+
+}  // namespace knn
+}  // namespace mepol
+
+using namespace mepol;
+using namespace mepol::knn;
+
+extern "C" int mepol_knn_workspace_size(int64_t n_cand, int64_t n_query, int d, int kp1,
+                                        int split_hint, size_t* bytes) {
+  Plan P;
+  int rc = make_plan(n_cand, n_query, d, kp1, split_hint, &P);
+  if (rc) return rc;
+  *bytes = P.total;
+  return 0;
+}
+
+extern "C" int mepol_knn_plan_info(int64_t n_cand, int64_t n_query, int d, int kp1,
+                                   int split_hint, int* ks, int* list, int* split) {
+  Plan P;
+  int rc = make_plan(n_cand, n_query, d, kp1, split_hint, &P);
+  if (rc) return rc;
+  if (ks) *ks = P.KS;
+  if (list) *list = P.LIST;
+  if (split) *split = P.split;
+  return 0;
+}
+
+extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, int64_t n_query,
+                         int d, int kp1, int split_hint, double* dist_out, int64_t* idx_out,
+                         int32_t* idx32_out, int32_t* n_fallback_out, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  Plan P;
+  int rc = make_plan(n_cand, n_query, d, kp1, split_hint, &P);
+  if (rc) return rc;
+  if (!cand || !query || !dist_out || !workspace) {
+    set_error("mepol_knn: null pointer argument");
+    return kErrBadArg;
+  }
+  if (workspace_bytes < P.total) {
+    set_error("mepol_knn: workspace %zu bytes < required %zu", workspace_bytes, P.total);
+    return kErrWorkspace;
+  }
+  if (n_query == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  char* ws = (char*)workspace;
+  float* apack = (float*)(ws + P.off_apack);
+  unsigned* cmax = (unsigned*)(ws + P.off_scalars);
+  int* fcount = n_fallback_out ? (int*)n_fallback_out : (int*)(ws + P.off_scalars + 4);
+  float* lv = (float*)(ws + P.off_lv);
+  int* li = (int*)(ws + P.off_li);
+  int* flist = (int*)(ws + P.off_flag);
+
+  MEPOL_HIP(hipMemsetAsync(ws + P.off_scalars, 0, 16, st));
+  if (n_fallback_out) MEPOL_HIP(hipMemsetAsync(n_fallback_out, 0, sizeof(int32_t), st));
+  {
+    const int64_t total = P.nct * 64;
+    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, cand,
+                       P.nc, P.d, P.KSP, P.nct, apack, cmax);
+    MEPOL_CHECK_LAUNCH();
+  }
+  {
+    dim3 g((unsigned)((P.nqt + 3) / 4), (unsigned)P.split);
+    switch (P.KS) {
+      case 2: launch_select_ks<2>(P, g, apack, query, lv, li, st); break;
+      case 4: launch_select_ks<4>(P, g, apack, query, lv, li, st); break;
+      case 8: launch_select_ks<8>(P, g, apack, query, lv, li, st); break;
+      case 12: launch_select_ks<12>(P, g, apack, query, lv, li, st); break;
+      case 15: launch_select_ks<15>(P, g, apack, query, lv, li, st); break;
+      case 16: launch_select_ks<16>(P, g, apack, query, lv, li, st); break;
+      case 24: launch_select_ks<24>(P, g, apack, query, lv, li, st); break;
+      default: launch_select_ks<32>(P, g, apack, query, lv, li, st); break;
+    }
+    MEPOL_CHECK_LAUNCH();
+  }
+  switch (P.LIST) {
+    case 8: launch_refine_list<8>(P, cand, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st); break;
+    case 16: launch_refine_list<16>(P, cand, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st); break;
+    case 40: launch_refine_list<40>(P, cand, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st); break;
+    default: launch_refine_list<64>(P, cand, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st); break;
+  }
+  MEPOL_CHECK_LAUNCH();
+  const unsigned eg = 512;
+  switch (P.LIST) {
+    case 8: launch_exact_list<8>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
+    case 16: launch_exact_list<16>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
+    case 40: launch_exact_list<40>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
+    default: launch_exact_list<64>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
+  }
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}
+
+// Exhaustive exact k-NN for every query (no fp32 selection): the reference semantics at the
+// cost of a full f64 scan.  Used for d > 63 / k+1 > 60 and as an independent check.
+extern "C" int mepol_knn_exact(const float* cand, int64_t n_cand, const float* query,
+                               int64_t n_query, int d, int kp1, double* dist_out, int64_t* idx_out,
+                               int32_t* idx32_out, int32_t* scratch_idx, void* stream) {
+  if (n_cand <= 0 || n_query < 0 || d <= 0 || kp1 <= 0 || kp1 > 64 || kp1 > n_cand ||
+      !scratch_idx) {
+    set_error("mepol_knn_exact: bad arguments (needs k+1 <= 64, k+1 <= n_cand, scratch)");
+    return kErrBadArg;
+  }
+  if (n_query == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  // scratch_idx: [1 + n_query] int32: count, then the identity query list.
+  Plan P{};
+  P.nc = n_cand;
+  P.d = d;
+  P.kp1 = kp1;
+  hipLaunchKernelGGL(fill_identity_kernel, dim3((unsigned)((n_query + 255) / 256)), dim3(256), 0, st, scratch_idx,
+                     n_query);
+  MEPOL_CHECK_LAUNCH();
+  const unsigned grid = (unsigned)std::min<int64_t>(n_query, 4096);
+  if (kp1 <= 8)
+    launch_exact_list<8>(P, cand, query, scratch_idx, scratch_idx + 1, dist_out, idx_out, idx32_out, grid, st);
+  else if (kp1 <= 16)
+    launch_exact_list<16>(P, cand, query, scratch_idx, scratch_idx + 1, dist_out, idx_out, idx32_out, grid, st);
+  else if (kp1 <= 40)
+    launch_exact_list<40>(P, cand, query, scratch_idx, scratch_idx + 1, dist_out, idx_out, idx32_out, grid, st);
+  else
+    launch_exact_list<64>(P, cand, query, scratch_idx, scratch_idx + 1, dist_out, idx_out, idx32_out, grid, st);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}

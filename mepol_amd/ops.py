@@ -1,0 +1,208 @@
+"""Torch-facing wrappers over the C ABI (device tensors in, device tensors out, current stream).
+
+Every function here launches HIP kernels from libmepol_amd.so; none has a CPU path.  Tensors
+must live on a ROCm device; dtypes follow the reference (f64 values, int64 indices at the
+API boundary; int32 indices internally).
+"""
+import math
+
+import torch
+
+from . import _lib
+from ._lib import call, ptr
+
+_WS = {}
+
+
+def _stream():
+    return ctypes_void(torch.cuda.current_stream().cuda_stream)
+
+
+def ctypes_void(v):
+    import ctypes
+
+    return ctypes.c_void_p(v)
+
+
+def _require_device(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("mepol_amd ops need ROCm device tensors (got a CPU tensor); "
+                             "there is no CPU path in the product")
+
+
+def _workspace(device, nbytes, tag="knn"):
+    key = (tag, device)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def knn_plan(n_cand, n_query, d, kp1, split=0):
+    import ctypes
+
+    ks, lst, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    call("mepol_knn_plan_info", n_cand, n_query, d, kp1, split, ctypes.byref(ks),
+         ctypes.byref(lst), ctypes.byref(sp))
+    return {"KS": ks.value, "LIST": lst.value, "split": sp.value}
+
+
+def knn(cand, kp1, query=None, split=0, want_int64=True, return_fallback=False):
+    """Exact k-NN of `query` rows among `cand` rows (both f32 [*, d] on device).
+
+    Returns (D f64 [nq, kp1], I int64 [nq, kp1] or None, I32T int32 [kp1, nq]) and, with
+    return_fallback, the device int32 count of queries that took the exhaustive path.
+    Replaces NearestNeighbors(k+1).fit(X).kneighbors(X) (src/algorithms/mepol.py:190-192).
+    """
+    import ctypes
+
+    if query is None:
+        query = cand
+    _require_device(cand, query)
+    cand = cand.contiguous().float()
+    query = query.contiguous().float()
+    nc, d = cand.shape
+    nq = query.shape[0]
+    if query.shape[1] != d:
+        raise ValueError("query/candidate dimension mismatch")
+    dev = cand.device
+    nbytes = ctypes.c_size_t()
+    call("mepol_knn_workspace_size", nc, nq, d, kp1, split, ctypes.byref(nbytes))
+    ws = _workspace(dev, nbytes.value)
+    D = torch.empty((nq, kp1), dtype=torch.float64, device=dev)
+    I = torch.empty((nq, kp1), dtype=torch.int64, device=dev) if want_int64 else None
+    I32T = torch.empty((kp1, nq), dtype=torch.int32, device=dev)
+    nfb = torch.zeros(1, dtype=torch.int32, device=dev)
+    call("mepol_knn", ptr(cand), nc, ptr(query), nq, d, kp1, split, ptr(D), ptr(I), ptr(I32T),
+         ptr(nfb), ptr(ws), ws.numel(), _stream())
+    if return_fallback:
+        return D, I, I32T, nfb
+    return D, I, I32T
+
+
+def knn_exact(cand, kp1, query=None, want_int64=True):
+    """Exhaustive f64 k-NN (every query scanned exactly); reference semantics, slower."""
+    if query is None:
+        query = cand
+    _require_device(cand, query)
+    cand = cand.contiguous().float()
+    query = query.contiguous().float()
+    nc, d = cand.shape
+    nq = query.shape[0]
+    dev = cand.device
+    D = torch.empty((nq, kp1), dtype=torch.float64, device=dev)
+    I = torch.empty((nq, kp1), dtype=torch.int64, device=dev) if want_int64 else None
+    I32T = torch.empty((kp1, nq), dtype=torch.int32, device=dev)
+    scratch = torch.empty(nq + 1, dtype=torch.int32, device=dev)
+    call("mepol_knn_exact", ptr(cand), nc, ptr(query), nq, d, kp1, ptr(D), ptr(I), ptr(I32T),
+         ptr(scratch), _stream())
+    return D, I, I32T
+
+
+def iw_forward(logp_t, logp_b, offsets, n_particles, normalize=True):
+    """u = exp(segmented cumsum(logp_t - logp_b)); w = u / sum(u).
+
+    logp_t/logp_b: f64 [nt, T_stride]; offsets: int64 [nt+1] particle offsets.
+    Returns (u [N], traj_sum [nt], w [N] or None, U 0-d or None).
+    """
+    _require_device(logp_t, logp_b, offsets)
+    nt, Ts = logp_t.shape
+    dev = logp_t.device
+    lt = logp_t.contiguous()
+    lb = logp_b.contiguous()
+    u = torch.empty(n_particles, dtype=torch.float64, device=dev)
+    ts = torch.empty(nt, dtype=torch.float64, device=dev)
+    w = torch.empty(n_particles, dtype=torch.float64, device=dev) if normalize else None
+    U = torch.empty((), dtype=torch.float64, device=dev) if normalize else None
+    call("mepol_iw_forward", ptr(lt), ptr(lb), nt, Ts, ptr(offsets), n_particles, ptr(u), ptr(ts),
+         ptr(w), ptr(U), _stream())
+    return u, ts, w, U
+
+
+def iw_normalize(u, U):
+    w = torch.empty_like(u)
+    call("mepol_iw_normalize", ptr(u), ptr(U), u.numel(), ptr(w), _stream())
+    return w
+
+
+def entropy_forward(w, idxT, D, k, ns, G, B, eps, n_w=None):
+    """Fused compute_entropy + compute_kl forward.
+
+    Returns (out4 f64[4] = {H, KL_unclamped, sum_term, sum_klterm}, W [n], g [n]).
+    """
+    _require_device(w, idxT, D)
+    n = D.shape[0]
+    kp1 = D.shape[1]
+    dev = w.device
+    if n_w is None:
+        n_w = w.numel()
+    nparts = _lib.load().mepol_entropy_partials_size(n)
+    partials = torch.empty(max(2 * nparts, 2), dtype=torch.float64, device=dev)
+    W = torch.empty(n, dtype=torch.float64, device=dev)
+    g = torch.empty(n, dtype=torch.float64, device=dev)
+    out4 = torch.empty(4, dtype=torch.float64, device=dev)
+    call("mepol_entropy_forward", ptr(w.contiguous()), ptr(idxT), ptr(D.contiguous()), n, n_w, k,
+         kp1, float(ns), float(G), float(B), float(eps), ptr(W), ptr(g), ptr(partials), ptr(out4),
+         _stream())
+    return out4, W, g
+
+
+def csr_build(idxT, k, n_own, col_offset=0, row_offset=0, nq=None):
+    """CSR transpose of the first k rows of idxT ([>=k, nq]) for ids [col_offset, +n_own)."""
+    _require_device(idxT)
+    if nq is None:
+        nq = idxT.shape[1]
+    dev = idxT.device
+    off = torch.empty(n_own + 1, dtype=torch.int32, device=dev)
+    rows = torch.empty(max(nq * k, 1), dtype=torch.int32, device=dev)
+    scratch = torch.empty(max(n_own, 1), dtype=torch.int32, device=dev)
+    call("mepol_csr_build", ptr(idxT), nq, k, col_offset, n_own, row_offset, ptr(off), ptr(rows),
+         ptr(scratch), _stream())
+    return off, rows
+
+
+def entropy_gamma(g, w_own, csr_off, csr_rows):
+    n_own = w_own.numel()
+    dev = w_own.device
+    gamma = torch.empty(n_own, dtype=torch.float64, device=dev)
+    nparts = (n_own + 255) // 256
+    partials = torch.empty(max(nparts, 1), dtype=torch.float64, device=dev)
+    call("mepol_entropy_gamma", ptr(g), ptr(w_own), ptr(csr_off), ptr(csr_rows), n_own,
+         ptr(gamma), ptr(partials), _stream())
+    return gamma, partials, nparts
+
+
+def entropy_reverse_scan(gamma, w, partials, nparts, offsets, nt, T_stride, grad_H, S_ext=None):
+    grad = torch.empty((nt, T_stride), dtype=torch.float64, device=w.device)
+    call("mepol_entropy_reverse_scan", ptr(gamma), ptr(w), ptr(partials), nparts, ptr(S_ext),
+         ptr(offsets), nt, T_stride, ptr(grad_H), ptr(grad), _stream())
+    return grad
+
+
+def step_mountaincar(state, action):
+    """In-place batched MountainCar step: state f64 [n,2], action f64 [n, a>=1]."""
+    _require_device(state, action)
+    call("mepol_step_mountaincar", ptr(state), ptr(action), state.shape[0], action.stride(0),
+         _stream())
+    return state
+
+
+def step_gridworld(state, action):
+    """In-place batched GridWorld step: state f32 [n,2], action f64 [n,2]."""
+    _require_device(state, action)
+    call("mepol_step_gridworld", ptr(state), ptr(action.contiguous()), state.shape[0], _stream())
+    return state
+
+
+def rollout_step(env_id, env_f64, env_f32, mean, noise, log_std, t, T, states_rec, actions_rec,
+                 policy_in):
+    n, a_dim = mean.shape
+    call("mepol_rollout_step", env_id, ptr(env_f64), ptr(env_f32), ptr(mean), ptr(noise),
+         ptr(log_std), n, a_dim, t, T, ptr(states_rec), ptr(actions_rec), ptr(policy_in),
+         _stream())
+
+
+def volume_constant(ns, G):
+    return math.pi ** (ns / 2) / G

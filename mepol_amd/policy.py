@@ -1,0 +1,98 @@
+"""GaussianPolicy with the reference's API and state-dict layout (src/policy.py:11-88).
+
+MLP ``net = [Linear(nf,h0), act, Linear(h0,h1), act, ...]``, ``mean = Linear(h_last, a)``,
+state-independent ``log_std`` parameter; keys ``net.0.*``, ``net.2.*``, ``mean.*``, ``log_std``
+(loadable from / by the reference, incl. its fp32 ``pretrained/*`` files).
+
+Parameters are float64 (the reference's dtype, src/utils/dtypes.py:3) and are initialised on
+the CPU generator in the reference's order (Linear defaults, then xavier_uniform on
+``mean.weight`` and the ``net`` weights, policy.py:36-41), so a given torch seed yields the
+reference's initial weights; the module can then be moved to the GPU with ``.to(device)``.
+The forward/backward runs on PyTorch-ROCm (hipBLASLt/rocBLAS GEMMs).
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+LOG_STD_EPS = 1e-7  # src/utils/dtypes.py:7, used inside get_log_p (policy.py:49)
+LOG_2PI = math.log(2 * math.pi)
+
+
+class GaussianPolicy(nn.Module):
+    def __init__(self, hidden_sizes, num_features, action_dim, log_std_init=-0.5,
+                 activation=nn.ReLU, dtype=torch.float64):
+        super().__init__()
+        self.activation = activation
+        self.num_features = num_features
+        self.action_dim = action_dim
+        widths = [num_features] + list(hidden_sizes)
+        layers = []
+        for fan_in, fan_out in zip(widths[:-1], widths[1:]):
+            layers += [nn.Linear(fan_in, fan_out, dtype=dtype), activation()]
+        self.net = nn.Sequential(*layers)
+        self.mean = nn.Linear(widths[-1], action_dim, dtype=dtype)
+        self.log_std = nn.Parameter(torch.full((action_dim,), float(log_std_init), dtype=dtype))
+        self.log_of_two_pi = LOG_2PI
+        self.initialize_weights()
+
+    def initialize_weights(self):
+        nn.init.xavier_uniform_(self.mean.weight)
+        for layer in self.net:
+            if isinstance(layer, nn.Linear):
+                nn.init.xavier_uniform_(layer.weight)
+
+    @property
+    def device(self):
+        return self.log_std.device
+
+    def mean_action(self, x):
+        return self.mean(self.net(x))
+
+    def get_log_p(self, states, actions):
+        """sum_a -0.5 (log 2pi + 2 log_std + (a - mu)^2 / (exp(log_std) + 1e-7)^2)."""
+        mu = self.mean_action(states)
+        std = torch.exp(self.log_std) + LOG_STD_EPS
+        return torch.sum(-0.5 * (self.log_of_two_pi + 2 * self.log_std + (actions - mu) ** 2 / std ** 2),
+                         dim=1)
+
+    def forward(self, x, deterministic=False):
+        mu = self.mean_action(x)
+        if deterministic:
+            return mu, mu
+        noise = torch.randn(mu.size(), dtype=mu.dtype, device=mu.device)
+        return mu, mu + noise * torch.exp(self.log_std)
+
+    def predict(self, s, deterministic=False):
+        """Batch-1 action for one state (policy.py:64-67); returned on the CPU as the reference."""
+        with torch.no_grad():
+            x = torch.as_tensor(s, dtype=self.log_std.dtype, device=self.device).unsqueeze(0)
+            return self(x, deterministic=deterministic)[1][0].cpu()
+
+
+def train_supervised(env, policy, train_steps=100, batch_size=5000):
+    """Regress the policy mean to zero on uniform observation-space states (policy.py:70-88).
+
+    As in the reference, every step draws 5000 fresh states (batch_size is not used,
+    Appendix A.10 of SURVEY.md) and Adam(lr=2.5e-4) is used.  Sampling is vectorised on the
+    policy's device when the env exposes a Box observation space.
+    """
+    optimizer = torch.optim.Adam(policy.parameters(), lr=0.00025)
+    space = env.observation_space
+    nf = env.num_features
+    for _ in range(train_steps):
+        optimizer.zero_grad()
+        if hasattr(space, "sample_torch"):
+            states = space.sample_torch(5000, policy.device)[:, :nf]
+        else:
+            obs = [space.sample() for _ in range(5000)]
+            if isinstance(obs[0], dict):
+                obs = [o["observation"] for o in obs]
+            else:
+                obs = [o[:nf] for o in obs]
+            states = torch.as_tensor(obs, dtype=torch.float64, device=policy.device)
+        mu = policy(states)[0]
+        loss = torch.mean((mu - torch.zeros_like(mu)) ** 2)
+        loss.backward()
+        optimizer.step()
+    return policy

@@ -1,0 +1,99 @@
+"""GPU env steppers and the fused rollout step vs the reference steps / oracle rollout."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, state_dict_from
+from oracle import mepol_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def test_gridworld_step_bitexact(cuda):
+    from mepol_amd import ops
+
+    z = load_golden("env_gw")
+    s = torch.as_tensor(z["S"], device="cuda").contiguous()
+    a = torch.as_tensor(z["A"], dtype=torch.float64, device="cuda")
+    ops.step_gridworld(s, a)
+    assert np.array_equal(s.cpu().numpy(), z["NS"])
+
+
+def test_mountaincar_step(cuda):
+    from mepol_amd import ops
+
+    z = load_golden("env_mc")
+    s = torch.as_tensor(z["S"], dtype=torch.float64, device="cuda").contiguous()
+    a = torch.as_tensor(z["A"], dtype=torch.float64, device="cuda")
+    ops.step_mountaincar(s, a)
+    got = s.cpu().numpy()
+    # cos() may differ from glibc in the last ulp; everything else is the same IEEE sequence
+    np.testing.assert_allclose(got, z["NS"], rtol=0, atol=1e-15)
+    assert (got == z["NS"]).mean() > 0.95
+
+
+@pytest.mark.parametrize("env", ["mountaincar", "gridworld"])
+def test_rollout_with_injected_noise_matches_oracle(cuda, env):
+    from mepol_amd import ops
+    from mepol_amd.policy import GaussianPolicy
+
+    torch.manual_seed(5)
+    a_dim = 1 if env == "mountaincar" else 2
+    pol = GaussianPolicy([32, 32], 2, a_dim, -0.5 if env == "mountaincar" else -1.5).cuda()
+    nt, T = 16, 200
+    rng = np.random.default_rng(0)
+    if env == "mountaincar":
+        init = np.stack([rng.uniform(-0.6, -0.4, nt), np.zeros(nt)], 1)
+    else:
+        init = rng.uniform(-6, -4, (nt, 2)).astype(np.float32)
+    noise = rng.standard_normal((T, nt, a_dim))
+    sd = {k: v.detach().cpu().numpy() for k, v in pol.state_dict().items()}
+    S_ref, A_ref = O.rollout(env, sd, sd["log_std"], init, noise, T)
+
+    dev = "cuda"
+    states = torch.zeros((nt, T + 1, 2), dtype=torch.float32, device=dev)
+    actions = torch.zeros((nt, T, a_dim), dtype=torch.float32, device=dev)
+    env_id = 0 if env == "mountaincar" else 1
+    init_t = torch.as_tensor(init, device=dev)
+    env64 = init_t.clone().double() if env_id == 0 else None
+    env32 = init_t.clone().float() if env_id == 1 else None
+    pin = init_t.double().contiguous()
+    states[:, 0] = init_t.float()
+    nz = torch.as_tensor(noise, dtype=torch.float64, device=dev)
+    with torch.no_grad():
+        for t in range(T):
+            mean = pol.mean_action(pin).contiguous()
+            ops.rollout_step(env_id, env64, env32, mean, nz[t].contiguous(), pol.log_std.detach(),
+                             t, T, states, actions, pin)
+    S = states.cpu().numpy()
+    A = actions.cpu().numpy()
+    # The MLP runs on rocBLAS (different summation order than numpy): actions agree to ~1e-15
+    # and the f32-recorded trajectories agree to f32 rounding unless a wall/clip boundary is
+    # crossed within that rounding (rare); require nearly every recorded value to match.
+    assert np.abs(A - A_ref).max() < 1e-5
+    frac_exact = (S == S_ref).mean()
+    assert frac_exact > 0.99, frac_exact
+    assert np.abs(S - S_ref).max() < 1e-3
+
+
+def test_collect_particles_contract(cuda):
+    """collect_particles_and_compute_knn returns the reference's shapes/dtypes (mepol.py:195-202)."""
+    from mepol_amd.algorithms import mepol as M
+    from mepol_amd.envs import ErgodicEnv, GridWorldContinuous
+    from mepol_amd.policy import GaussianPolicy
+
+    torch.manual_seed(0)
+    env = ErgodicEnv(GridWorldContinuous())
+    pol = GaussianPolicy([300, 300], 2, 2, -1.5).cuda()
+    st, ac, rl, ns, D, I = M.collect_particles_and_compute_knn(env, pol, 20, 1000, None, 4, 1)
+    assert st.shape == (20, 1001, 2) and st.dtype == torch.float64
+    assert ac.shape == (20, 1000, 2) and ac.dtype == torch.float64
+    assert rl.shape == (20, 1) and rl.dtype == torch.int64 and bool((rl == 1000).all())
+    assert ns.shape == (20000, 2) and ns.dtype == torch.float64
+    assert D.shape == (20000, 5) and D.dtype == torch.float64
+    assert I.shape == (20000, 5) and I.dtype == torch.int64
+    # states stay inside the grid and off the walls; next_states are states[:, 1:]
+    assert bool((st.abs() < 6).all())
+    assert torch.equal(ns, st[:, 1:].reshape(-1, 2))
+    Do, Io = O.knn_exact(ns.float().cpu().numpy(), 5)
+    assert np.array_equal(D.cpu().numpy(), Do) and np.array_equal(I.cpu().numpy(), Io)

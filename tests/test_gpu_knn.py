@@ -1,0 +1,109 @@
+"""GPU k-NN parity (calls through the C ABI): reference fixtures + oracle at other sizes."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from oracle import mepol_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+KNN_TIE_FREE = ["knn_mc_d2", "knn_d7", "knn_ant_d29", "knn_hum_d47", "knn_hr_d63", "knn_d30_k30"]
+
+
+def _knn(X, kp1, **kw):
+    from mepol_amd import ops
+
+    Xt = torch.as_tensor(np.ascontiguousarray(X), dtype=torch.float32, device="cuda")
+    D, I, I32T, nfb = ops.knn(Xt, kp1, return_fallback=True, **kw)
+    torch.cuda.synchronize()
+    return D.cpu().numpy(), I.cpu().numpy(), I32T.cpu().numpy(), int(nfb.item())
+
+
+@pytest.mark.parametrize("name", KNN_TIE_FREE)
+def test_knn_matches_reference_fixture(cuda, name):
+    z = load_golden(name)
+    D, I, I32T, _ = _knn(z["X"], int(z["kp1"]))
+    np.testing.assert_allclose(D, z["D"], rtol=4e-16, atol=0)
+    assert np.array_equal(I, z["I"].astype(np.int64))
+    assert np.array_equal(I32T.T, I)
+
+
+@pytest.mark.parametrize("name", KNN_TIE_FREE + ["knn_gw_ties", "knn_gw_c2"])
+def test_knn_bitexact_vs_oracle(cuda, name):
+    """Same f64 arithmetic and the same (distance, index) tie-break as the oracle: bit-exact."""
+    z = load_golden(name)
+    kp1 = int(z["kp1"])
+    D, I, _, _ = _knn(z["X"], kp1)
+    Do, Io = O.knn_exact(z["X"], kp1)
+    assert np.array_equal(D, Do)
+    assert np.array_equal(I, Io)
+
+
+@pytest.mark.parametrize("split", [1, 3, 16])
+def test_knn_split_invariance(cuda, split):
+    z = load_golden("knn_ant_d29")
+    D0, I0, _, _ = _knn(z["X"], 31)
+    D1, I1, _, _ = _knn(z["X"], 31, split=split)
+    assert np.array_equal(D0, D1) and np.array_equal(I0, I1)
+
+
+@pytest.mark.parametrize("n,d,kp1", [(1, 3, 1), (7, 1, 7), (33, 5, 33), (1000, 63, 51),
+                                     (4097, 29, 31), (3001, 12, 5), (2500, 24, 60)])
+def test_knn_edge_shapes(cuda, n, d, kp1):
+    X = np.random.default_rng(n + d).standard_normal((n, d)).astype(np.float32)
+    D, I, _, _ = _knn(X, kp1)
+    Do, Io = O.knn_exact(X, kp1)
+    assert np.array_equal(D, Do)
+    assert np.array_equal(I, Io)
+
+
+def test_knn_all_duplicates_uses_exact_path(cuda):
+    X = np.zeros((500, 3), np.float32)
+    X[250:] = 1.0
+    D, I, _, nfb = _knn(X, 5)
+    Do, Io = O.knn_exact(X, 5)
+    assert nfb > 0
+    assert np.array_equal(D, Do) and np.array_equal(I, Io)
+
+
+def test_knn_query_shard_matches_full(cuda):
+    """Multi-rank form: a query shard against all candidates == rows of the full result."""
+    from mepol_amd import ops
+
+    X = np.random.default_rng(3).standard_normal((3000, 29)).astype(np.float32)
+    Xt = torch.as_tensor(X, device="cuda")
+    Df, If, _ = ops.knn(Xt, 31)
+    Ds, Is, _ = ops.knn(Xt, 31, query=Xt[1000:2200])
+    assert torch.equal(Df[1000:2200], Ds) and torch.equal(If[1000:2200], Is)
+
+
+def test_knn_exact_path_matches_oracle(cuda):
+    from mepol_amd import ops
+
+    z = load_golden("knn_gw_ties")
+    Xt = torch.as_tensor(z["X"], device="cuda")
+    D, I, _ = ops.knn_exact(Xt, 5)
+    Do, Io = O.knn_exact(z["X"], 5)
+    assert np.array_equal(D.cpu().numpy(), Do) and np.array_equal(I.cpu().numpy(), Io)
+
+
+def test_knn_large_properties(cuda):
+    """BASELINE-size batch (N=200k, d=29, k=30): properties that need no CPU oracle."""
+    from mepol_amd import ops
+
+    g = torch.Generator(device="cuda").manual_seed(0)
+    X = torch.randn((200000, 29), device="cuda", generator=g, dtype=torch.float32)
+    D, I, I32T, nfb = ops.knn(X, 31, return_fallback=True)
+    torch.cuda.synchronize()
+    assert bool((D[:, 1:] >= D[:, :-1]).all())                  # rows sorted
+    assert bool((I[:, 0] == torch.arange(200000, device="cuda")).all())  # self first (tie-free)
+    # recomputed distances agree with the reported ones
+    sel = torch.randint(0, 200000, (2000,), device="cuda", generator=g)
+    Xd = X.double()
+    dd = ((Xd[sel][:, None, :] - Xd[I[sel]]) ** 2).sum(-1).sqrt()
+    assert torch.allclose(dd, D[sel], rtol=1e-14, atol=0)
+    # a sampled subset checked exhaustively against the exact path
+    Dq, Iq, _ = ops.knn_exact(X, 31, query=X[sel[:64]])
+    assert torch.equal(Dq, D[sel[:64]]) and torch.equal(Iq, I[sel[:64]])
+    assert int(nfb.item()) < 200  # certification almost never needs the exhaustive path

@@ -1,0 +1,138 @@
+"""Pin the CPU oracle (oracle/mepol_oracle.py) against the reference's own outputs.
+
+The golden fixtures were produced by running the reference implementation
+(tests/golden/make_golden.py); if the oracle agrees with them, the GPU parity tests that use
+the oracle at other sizes inherit the reference's semantics.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden, state_dict_from
+from oracle import mepol_oracle as O
+
+KNN_TIE_FREE = ["knn_mc_d2", "knn_d7", "knn_ant_d29", "knn_hum_d47", "knn_hr_d63", "knn_d30_k30"]
+ENTROPY = ["entropy_gw", "entropy_mc", "entropy_ant", "entropy_ant_d29", "entropy_gw300",
+           "entropy_dup_inf"]
+
+
+@pytest.mark.parametrize("name", KNN_TIE_FREE)
+def test_knn_oracle_matches_reference(name):
+    z = load_golden(name)
+    D, I = O.knn_exact(z["X"], int(z["kp1"]))
+    # sklearn kd_tree computes the same f64 sum of squares: distances agree to the last ulp or so
+    np.testing.assert_allclose(D, z["D"], rtol=4e-16, atol=1e-300)
+    assert np.array_equal(I, z["I"].astype(np.int64))
+
+
+@pytest.mark.parametrize("name", ["knn_gw_ties", "knn_gw_c2"])
+def test_knn_oracle_ties_tie_invariant(name):
+    """Real GridWorld particles have exact duplicates: compare what tie order cannot change."""
+    z = load_golden(name)
+    X = z["X"]
+    D, I = O.knn_exact(X, int(z["kp1"]))
+    np.testing.assert_allclose(D, z["D"], rtol=4e-16, atol=0)
+    Ir = z["I"].astype(np.int64)
+    # every returned neighbour is at the reported distance (for both), and index sets agree
+    # except inside a tie group straddling the last column
+    Xd = X.astype(np.float64)
+    for arr in (I, Ir):
+        dd = np.sqrt(((Xd[:, None, :] - Xd[arr]) ** 2).sum(-1))
+        np.testing.assert_allclose(dd, D, rtol=1e-12, atol=1e-12)
+    last = D[:, -1:]
+    strict_ours = [set(r[d < l[0]]) for r, d, l in zip(I, D, last)]
+    strict_ref = [set(r[d < l[0]]) for r, d, l in zip(Ir, D, last)]
+    assert strict_ours == strict_ref
+
+
+@pytest.mark.parametrize("name", ["policy_gw", "policy_ant", "policy_pretrained_gw"])
+def test_policy_logp(name):
+    z = load_golden(name)
+    sd = state_dict_from(z, "sd.")
+    np.testing.assert_allclose(O.mlp_mean(sd, z["x"]), z["mean"], rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(O.log_p(sd, z["x"], z["a"]), z["logp"], rtol=1e-12, atol=1e-12)
+
+
+def _entropy_inputs(z, it):
+    beh = state_dict_from(z, "beh.")
+    tgt = state_dict_from(z, f"it{it}.tgt.")
+    S, A = z["states"].astype(np.float64), z["actions"].astype(np.float64)
+    nt, T = A.shape[:2]
+    flat_s = S[:, :T].reshape(nt * T, -1)
+    flat_a = A.reshape(nt * T, -1)
+    lt = O.log_p(tgt, flat_s, flat_a).reshape(nt, T)
+    lb = O.log_p(beh, flat_s, flat_a).reshape(nt, T)
+    lengths = z["rtl"].reshape(-1).tolist()
+    return lt, lb, lengths
+
+
+@pytest.mark.parametrize("name", ENTROPY)
+def test_entropy_kl_oracle(name):
+    z = load_golden(name)
+    k, eps, G, B, ns = int(z["k"]), float(z["eps"]), float(z["G"]), float(z["B"]), int(z["ns"])
+    D, I = z["D"], z["I"].astype(np.int64)
+    for it in range(3):
+        lt, lb, lengths = _entropy_inputs(z, it)
+        w = O.importance_weights(lt, lb, lengths)
+        gw = z[f"it{it}.w"]
+        if np.all(np.isfinite(gw)):
+            np.testing.assert_allclose(w, gw, rtol=1e-10, atol=1e-300)
+        H = O.entropy(w, D, I, k, G, B, ns, eps)
+        gH = float(z[f"it{it}.H"])
+        if np.isfinite(gH):
+            assert abs(H - gH) <= 1e-10 * max(1.0, abs(gH))
+        else:
+            assert not np.isfinite(H)
+    # KL after each step uses the next iterate's parameters
+    for it in range(3):
+        nxt = f"it{it + 1}.tgt." if it < 2 else "final.tgt."
+        beh = state_dict_from(z, "beh.")
+        tgt = state_dict_from(z, nxt)
+        S, A = z["states"].astype(np.float64), z["actions"].astype(np.float64)
+        nt, T = A.shape[:2]
+        fs, fa = S[:, :T].reshape(nt * T, -1), A.reshape(nt * T, -1)
+        w = O.importance_weights(O.log_p(tgt, fs, fa).reshape(nt, T),
+                                 O.log_p(beh, fs, fa).reshape(nt, T), z["rtl"].reshape(-1).tolist())
+        kl, err, _ = O.kl(w, I, k, eps)
+        assert err == bool(z[f"it{it}.kerr"])
+        gk = float(z[f"it{it}.kl"])
+        if np.isfinite(gk):
+            assert abs(kl - gk) <= 1e-9 * max(1.0, abs(gk))
+
+
+@pytest.mark.parametrize("name", [n for n in ENTROPY if n != "entropy_dup_inf"])
+def test_entropy_closed_form_gradient(name):
+    """Closed-form dH/dlogp pushed through the MLP == the reference autograd param grads."""
+    z = load_golden(name)
+    k, eps, G, ns = int(z["k"]), float(z["eps"]), float(z["G"]), int(z["ns"])
+    D, I = z["D"], z["I"].astype(np.int64)
+    it = 0
+    lt, lb, lengths = _entropy_inputs(z, it)
+    if not np.isfinite(float(z[f"it{it}.H"])):
+        pytest.skip("non-finite entropy")
+    w = O.importance_weights(lt, lb, lengths)
+    c = O.entropy_grad_logp(w, D, I, k, G, ns, eps, lengths)
+    tgt = state_dict_from(z, f"it{it}.tgt.")
+    hidden = [tgt[f"net.{i}.weight"].shape[0] for i in range(0, 100, 2) if f"net.{i}.weight" in tgt]
+    nf = tgt["net.0.weight"].shape[1]
+    a = tgt["mean.weight"].shape[0]
+    pol = O.TorchPolicy(hidden, nf, a)
+    pol.load_state_dict({kk: torch.as_tensor(v) for kk, v in tgt.items()})
+    S = torch.as_tensor(z["states"], dtype=torch.float64)
+    A = torch.as_tensor(z["actions"], dtype=torch.float64)
+    nt, T = A.shape[:2]
+    logp = pol.get_log_p(S[:, :T].reshape(nt * T, -1), A.reshape(nt * T, -1)).reshape(nt, T)
+    # loss = -H  ->  dloss/dtheta = -sum c * dlogp/dtheta
+    (-(torch.as_tensor(c) * logp).sum()).backward()
+    for pname, p in pol.named_parameters():
+        ref = z[f"it{it}.grad.{pname}"]
+        got = p.grad.numpy()
+        scale = np.abs(ref).max() + 1e-300
+        assert np.abs(got - ref).max() <= 1e-9 * scale, pname
+
+
+def test_env_steps_oracle():
+    z = load_golden("env_mc")
+    np.testing.assert_allclose(O.mountaincar_step(z["S"], z["A"]), z["NS"], rtol=0, atol=1e-15)
+    z = load_golden("env_gw")
+    assert np.array_equal(O.gridworld_step(z["S"], z["A"]), z["NS"])
