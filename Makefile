@@ -2,7 +2,7 @@
 # optional C helpers.  `make -j8` here; the .so travels to the GPU box with the snapshot.
 HIPCC   ?= /opt/rocm/bin/hipcc
 ARCH    ?= gfx950
-FLAGS   := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result
+FLAGS   := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-result
 SRC     := $(wildcard mepol_amd/csrc/*.hip)
 OBJ     := $(patsubst mepol_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB     := mepol_amd/libmepol_amd.so

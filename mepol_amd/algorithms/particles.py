@@ -15,7 +15,8 @@ import torch
 
 from .. import ops
 
-_REGISTRY = weakref.WeakKeyDictionary()
+# indices-tensor identity -> ParticleBatch (entries vanish with the tensor; identity, not ==)
+_REGISTRY = {}
 
 
 def _param_key(policy):
@@ -80,16 +81,18 @@ class ParticleBatch:
 
 
 def register(indices, batch):
-    _REGISTRY[indices] = batch
+    key = id(indices)
+    if key not in _REGISTRY:
+        weakref.finalize(indices, _REGISTRY.pop, key, None)
+    _REGISTRY[key] = batch
     return batch
 
 
 def lookup(states, actions, real_traj_lengths, distances, indices):
     """The registered batch for these tensors, or a new one built from them."""
-    b = _REGISTRY.get(indices)
+    b = _REGISTRY.get(id(indices))
     if b is not None and b.kp1 == distances.shape[1] and b.num_traj == actions.shape[0] and (
             b.D.data_ptr() == distances.data_ptr() or torch.equal(b.D, distances.to(b.device))):
         return b
     b = ParticleBatch(states, actions, real_traj_lengths, distances, indices)
-    _REGISTRY[indices] = b
-    return b
+    return register(indices, b)

@@ -240,6 +240,20 @@ __device__ __forceinline__ double exact_d2(const float* __restrict__ a, const fl
   return s;
 }
 
+// Correctly rounded f64 square root (round-to-nearest-even, as glibc / numpy / sklearn).
+// y0 = sqrt(x) is within 1 ulp; with Y = y/ulp(y) an integer, x/ulp^2 is an integer, so
+// "RN(sqrt x) >= y+"  <=>  x > y*y+  and  "RN(sqrt x) <= y-"  <=>  x <= y-*y; both signs are
+// exact through one fma (a rounded nonzero keeps its sign).
+__device__ __forceinline__ double sqrt_rn(double x) {
+  const double y = sqrt(x);
+  if (!(x > 1e-290) || !(x < 1e300)) return y;
+  const double yp = __longlong_as_double(__double_as_longlong(y) + 1);
+  if (__builtin_fma(-y, yp, x) > 0.0) return yp;
+  const double ym = __longlong_as_double(__double_as_longlong(y) - 1);
+  if (__builtin_fma(-ym, y, x) <= 0.0) return ym;
+  return y;
+}
+
 template <int LIST, int MAXP>
 __global__ __launch_bounds__(256) void refine_kernel(
     const float* __restrict__ cand, int64_t nc, const float* __restrict__ query, int64_t nq, int d,
@@ -349,9 +363,9 @@ __global__ __launch_bounds__(256) void refine_kernel(
   bool ok = (eki != INT_MAX);
   if (bnd < 1e29f) ok = ok && (ek < ((double)bnd + qn2) - E);
   if (l < kp1) {
-    Dout[q * kp1 + l] = sqrt(dd);
+    Dout[q * kp1 + l] = sqrt_rn(dd);
     if (I64) I64[q * kp1 + l] = di;
-    if (I32) I32[q * kp1 + l] = di;
+    if (I32) I32[(int64_t)l * nq + q] = di;  // transposed [kp1][nq]
   }
   if (!ok && l == 0) {
     const int slot = atomicAdd(flag_count, 1);
@@ -364,7 +378,8 @@ __global__ __launch_bounds__(256) void refine_kernel(
 // ---------------------------------------------------------------------------------------
 template <int LIST>
 __global__ __launch_bounds__(256) void exact_kernel(const float* __restrict__ cand, int64_t nc,
-                                                    const float* __restrict__ query, int d, int kp1,
+                                                    const float* __restrict__ query, int64_t nq,
+                                                    int d, int kp1,
                                                     const int* __restrict__ flag_count,
                                                     const int* __restrict__ flag_list,
                                                     double* __restrict__ Dout,
@@ -440,9 +455,9 @@ __global__ __launch_bounds__(256) void exact_kernel(const float* __restrict__ ca
         li[LIST - 1] = INT_MAX;
       }
       if (tid == 0) {
-        Dout[q * kp1 + r] = sqrt(bd);
+        Dout[q * kp1 + r] = sqrt_rn(bd);
         if (I64) I64[q * kp1 + r] = bi;
-        if (I32) I32[q * kp1 + r] = bi;
+        if (I32) I32[(int64_t)r * nq + q] = bi;  // transposed [kp1][nq]
       }
     }
   }
@@ -585,8 +600,8 @@ template <int LIST>
 static void launch_exact_list(const Plan& P, const float* cand, const float* query, const int* fc,
                               const int* fl, double* D, int64_t* I64, int32_t* I32,
                               unsigned grid, hipStream_t st) {
-  hipLaunchKernelGGL((exact_kernel<LIST>), dim3(grid), dim3(256), 0, st, cand, P.nc, query, P.d,
-                     P.kp1, fc, fl, D, I64, I32);
+  hipLaunchKernelGGL((exact_kernel<LIST>), dim3(grid), dim3(256), 0, st, cand, P.nc, query, P.nq,
+                     P.d, P.kp1, fc, fl, D, I64, I32);
 }
 
 }  // namespace knn
@@ -695,6 +710,7 @@ extern "C" int mepol_knn_exact(const float* cand, int64_t n_cand, const float* q
   // scratch_idx: [1 + n_query] int32: count, then the identity query list.
   Plan P{};
   P.nc = n_cand;
+  P.nq = n_query;
   P.d = d;
   P.kp1 = kp1;
   hipLaunchKernelGGL(fill_identity_kernel, dim3((unsigned)((n_query + 255) / 256)), dim3(256), 0, st, scratch_idx,

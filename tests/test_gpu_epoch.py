@@ -9,7 +9,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("env,k", [("GridWorld", 4), ("MountainCar", 4)])
+@pytest.mark.parametrize("env,k", [("GridWorld", 50), ("MountainCar", 4)])
 def test_cli_epochs(cuda, tmp_path, env, k):
     from mepol_amd.experiments.mepol import main
 
