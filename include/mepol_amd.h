@@ -85,10 +85,12 @@ int mepol_entropy_forward(const double* w, const int32_t* idxT, const double* D,
                           void* stream);
 
 /* ---- entropy gradient (the autograd of policy_update's loss.backward(), mepol.py:278) ----
- * CSR transpose of the first k rows of idxT for owned ids [col_offset, col_offset + ncand). */
+ * CSR transpose of the first k rows of idxT ([>=k, nq]) for owned ids [col_offset, +ncand):
+ * csr_off [ncand+1], csr_rows [nq*k] (query rows row_offset + i, stable order). */
+int mepol_csr_workspace_size(int64_t nq, int k, int64_t ncand, size_t* bytes);
 int mepol_csr_build(const int32_t* idxT, int64_t nq, int k, int64_t col_offset, int64_t ncand,
-                    int64_t row_offset, int32_t* csr_off, int32_t* csr_rows, int32_t* scratch,
-                    void* stream);
+                    int64_t row_offset, int32_t* csr_off, int32_t* csr_rows, void* workspace,
+                    size_t workspace_bytes, void* stream);
 /* gamma_j = sum_{i in CSR(j)} g_i ; partials[b] = block sums of gamma_j w_j. */
 int mepol_entropy_gamma(const double* g, const double* w_own, const int32_t* csr_off,
                         const int32_t* csr_rows, int64_t n_own, double* gamma_out,

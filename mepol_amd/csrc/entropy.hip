@@ -165,69 +165,6 @@ __global__ __launch_bounds__(256) void entropy_finalize_kernel(const double* __r
 // ---------------------------------------------------------------------------------------
 // CSR transpose of I[:, :k] (built once per epoch: indices are fixed within an epoch).
 // ---------------------------------------------------------------------------------------
-// Candidate ids j are global; this CSR covers the owned range [col_offset, col_offset+ncand).
-__global__ void csr_count_kernel(const int32_t* __restrict__ idxT, int64_t nq, int k,
-                                 int64_t col_offset, int64_t ncand, int32_t* __restrict__ count) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= nq * (int64_t)k) return;
-  const int64_t j = (int64_t)idxT[e] - col_offset;  // idxT is [>=k][nq]: first k rows contiguous
-  if (j >= 0 && j < ncand) atomicAdd(&count[j], 1);
-}
-
-// Single-block exclusive scan of count[0..n) into off[0..n] (off[n] = total).
-__global__ __launch_bounds__(1024) void scan_kernel(const int32_t* __restrict__ count, int64_t n,
-                                                    int32_t* __restrict__ off) {
-  __shared__ int64_t sh[1024];
-  const int tid = threadIdx.x;
-  const int64_t chunk = (n + 1023) / 1024;
-  const int64_t b = tid * chunk, e = min(n, b + chunk);
-  int64_t s = 0;
-  for (int64_t i = b; i < e; ++i) s += count[i];
-  sh[tid] = s;
-  __syncthreads();
-  for (int m = 1; m < 1024; m <<= 1) {
-    int64_t v = (tid >= m) ? sh[tid - m] : 0;
-    __syncthreads();
-    sh[tid] += v;
-    __syncthreads();
-  }
-  int64_t run = sh[tid] - s;
-  for (int64_t i = b; i < e; ++i) {
-    off[i] = (int32_t)run;
-    run += count[i];
-  }
-  if (tid == 1023) off[n] = (int32_t)sh[1023];
-}
-
-__global__ void csr_fill_kernel(const int32_t* __restrict__ idxT, int64_t nq, int k,
-                                int64_t col_offset, int64_t ncand, int64_t row_offset,
-                                const int32_t* __restrict__ off, int32_t* __restrict__ cursor,
-                                int32_t* __restrict__ rows) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= nq * (int64_t)k) return;
-  const int64_t j = (int64_t)idxT[e] - col_offset;
-  if (j < 0 || j >= ncand) return;
-  const int64_t i = e % nq;
-  const int32_t pos = off[j] + atomicAdd(&cursor[j], 1);
-  rows[pos] = (int32_t)(i + row_offset);
-}
-
-// Sort each segment ascending so gamma sums in a fixed order (bitwise-reproducible).
-__global__ void csr_sort_kernel(const int32_t* __restrict__ off, int64_t n, int32_t* __restrict__ rows) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const int32_t b = off[j], e = off[j + 1];
-  for (int32_t x = b + 1; x < e; ++x) {
-    const int32_t v = rows[x];
-    int32_t y = x - 1;
-    while (y >= b && rows[y] > v) {
-      rows[y + 1] = rows[y];
-      --y;
-    }
-    rows[y + 1] = v;
-  }
-}
-
 // ---------------------------------------------------------------------------------------
 // Backward.
 // ---------------------------------------------------------------------------------------
@@ -355,38 +292,6 @@ extern "C" int mepol_entropy_forward(const double* w, const int32_t* idxT, const
     MEPOL_CHECK_LAUNCH();
   }
   hipLaunchKernelGGL(entropy_finalize_kernel, dim3(1), dim3(256), 0, st, partials, nb, B, n_w, out4);
-  MEPOL_CHECK_LAUNCH();
-  return 0;
-}
-
-// CSR transpose of the first k rows of idxT ([>=k][nq]): for every owned candidate id
-// j in [col_offset, col_offset + ncand) the sorted list of query rows (row_offset + i) whose
-// first k neighbours contain j.  csr_off: [ncand+1]; csr_rows: [nq*k]; scratch: [ncand] int32.
-extern "C" int mepol_csr_build(const int32_t* idxT, int64_t nq, int k, int64_t col_offset,
-                               int64_t ncand, int64_t row_offset, int32_t* csr_off,
-                               int32_t* csr_rows, int32_t* scratch, void* stream) {
-  if (!idxT || !csr_off || !csr_rows || !scratch || k <= 0 || ncand <= 0) {
-    set_error("mepol_csr_build: bad arguments");
-    return kErrBadArg;
-  }
-  hipStream_t st = (hipStream_t)stream;
-  const int64_t ne = nq * (int64_t)k;
-  MEPOL_HIP(hipMemsetAsync(scratch, 0, ncand * sizeof(int32_t), st));
-  if (ne > 0) {
-    hipLaunchKernelGGL(csr_count_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, idxT,
-                       nq, k, col_offset, ncand, scratch);
-    MEPOL_CHECK_LAUNCH();
-  }
-  hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, scratch, ncand, csr_off);
-  MEPOL_CHECK_LAUNCH();
-  MEPOL_HIP(hipMemsetAsync(scratch, 0, ncand * sizeof(int32_t), st));
-  if (ne > 0) {
-    hipLaunchKernelGGL(csr_fill_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st, idxT,
-                       nq, k, col_offset, ncand, row_offset, csr_off, scratch, csr_rows);
-    MEPOL_CHECK_LAUNCH();
-  }
-  hipLaunchKernelGGL(csr_sort_kernel, dim3((unsigned)((ncand + 255) / 256)), dim3(256), 0, st,
-                     csr_off, ncand, csr_rows);
   MEPOL_CHECK_LAUNCH();
   return 0;
 }

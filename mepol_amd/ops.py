@@ -151,15 +151,19 @@ def entropy_forward(w, idxT, D, k, ns, G, B, eps, n_w=None):
 
 def csr_build(idxT, k, n_own, col_offset=0, row_offset=0, nq=None):
     """CSR transpose of the first k rows of idxT ([>=k, nq]) for ids [col_offset, +n_own)."""
+    import ctypes
+
     _require_device(idxT)
     if nq is None:
         nq = idxT.shape[1]
     dev = idxT.device
+    nbytes = ctypes.c_size_t()
+    call("mepol_csr_workspace_size", nq, k, n_own, ctypes.byref(nbytes))
+    ws = _workspace(dev, nbytes.value, tag="csr")
     off = torch.empty(n_own + 1, dtype=torch.int32, device=dev)
     rows = torch.empty(max(nq * k, 1), dtype=torch.int32, device=dev)
-    scratch = torch.empty(max(n_own, 1), dtype=torch.int32, device=dev)
     call("mepol_csr_build", ptr(idxT), nq, k, col_offset, n_own, row_offset, ptr(off), ptr(rows),
-         ptr(scratch), _stream())
+         ptr(ws), ws.numel(), _stream())
     return off, rows
 
 
