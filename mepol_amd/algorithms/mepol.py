@@ -456,13 +456,18 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
 def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_valid_target_policy,
                             states, actions, num_traj, real_traj_lengths, distances, indices, k, G,
                             B, ns, eps, kl_threshold, max_off_iters, use_backtracking,
-                            backtrack_coeff, max_backtrack_try, original_lr, on_accept=None):
+                            backtrack_coeff, max_backtrack_try, original_lr, on_accept=None,
+                            fns=None):
     """The off-policy loop of one epoch with KL acceptance and backtracking (mepol.py:416-483).
 
     Returns (final entropy of the last valid target as a 0-d tensor, num_off_iters,
     backtrack_iter, learning_rate).  last_valid_target_policy must hold the behavioral
-    parameters on entry (mepol.py:409).
+    parameters on entry (mepol.py:409).  `fns` optionally supplies policy_update / compute_kl /
+    compute_entropy with this module's signatures (the sharded multi-rank epoch does).
     """
+    import sys
+
+    fns = fns if fns is not None else sys.modules[__name__]
     kl_threshold_reached = False
     num_off_iters = 0
     learning_rate = original_lr
@@ -474,12 +479,13 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
         backtrack_iter = None
 
     while not kl_threshold_reached:
-        loss, numeric_error = policy_update(optimizer, behavioral_policy, target_policy, states,
-                                            actions, num_traj, real_traj_lengths, distances,
-                                            indices, k, G, B, ns, eps)
+        loss, numeric_error = fns.policy_update(optimizer, behavioral_policy, target_policy, states,
+                                                actions, num_traj, real_traj_lengths, distances,
+                                                indices, k, G, B, ns, eps)
         entropy = -_np(loss)
-        kl, kl_numeric_error = compute_kl(behavioral_policy, target_policy, states, actions,
-                                          num_traj, real_traj_lengths, distances, indices, k, eps)
+        kl, kl_numeric_error = fns.compute_kl(behavioral_policy, target_policy, states, actions,
+                                              num_traj, real_traj_lengths, distances, indices, k,
+                                              eps)
         kl = _np(kl)
 
         if not numeric_error and not kl_numeric_error and kl <= kl_threshold:
@@ -504,9 +510,9 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
             kl_threshold_reached = True
 
     with torch.no_grad():
-        entropy = compute_entropy(last_valid_target_policy, last_valid_target_policy, states,
-                                  actions, num_traj, real_traj_lengths, distances, indices, k, G,
-                                  B, ns, eps)
+        entropy = fns.compute_entropy(last_valid_target_policy, last_valid_target_policy, states,
+                                      actions, num_traj, real_traj_lengths, distances, indices, k,
+                                      G, B, ns, eps)
     return entropy, num_off_iters, backtrack_iter, learning_rate
 
 

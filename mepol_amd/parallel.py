@@ -1,0 +1,212 @@
+"""Particle-batch data parallelism over ranks (one process per GPU, RCCL over xGMI).
+
+The reference scales the rollout with joblib worker processes (src/algorithms/mepol.py:179-187)
+and the k-NN with sklearn threads (:190); everything else is one process.  Here the particle
+batch is sharded by trajectory over `world` ranks (rank r owns trajectories
+[r*nt/G, (r+1)*nt/G) = particles [R0, R1) in the reference's traj-major order):
+
+  once per epoch   all-gather next-states (f32)            -> every rank holds all N candidates
+                   k-NN of the rank's own queries           -> D, I for particles [R0, R1)
+                   all-gather I[:, :k] (int32)              -> CSR of "who has me as neighbour"
+                                                               for the rank's own particles
+  per forward      sum of u: all-gather G partial sums      (fixed-order sum, identical bits)
+                   all-gather w                             (N f64: the gather reads any index)
+                   entropy/KL raw sums: all-gather G pairs
+  per backward     all-gather g = dH/dW                      (N f64)
+                   S = sum gamma_j w_j: all-gather G partials
+                   policy gradients: one all-reduce of the flattened f64 grads
+so every rank holds the same H, KL and parameters and takes the same accept/backtrack branch
+(mepol.py:441-476).  Payloads are 1.6 MB per vector at N = 200k: latency-bound on xGMI.
+
+The kernels come from `ops` (the HIP library).  Tests may inject another object with the same
+functions to check this module's collective algebra on CPU with the gloo backend.
+"""
+import torch
+
+from . import ops as _hip_ops
+
+
+class ShardedEpoch:
+    def __init__(self, states, actions, real_traj_lengths, next_states_f32, k, dist, group=None,
+                 ops=None):
+        self.dist = dist
+        self.group = group
+        self.ops = ops if ops is not None else _hip_ops
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.states = states
+        self.actions = actions
+        self.nt, self.T = actions.shape[0], actions.shape[1]
+        self.dev = states.device
+        lens = real_traj_lengths.reshape(-1).to(torch.int64).cpu()
+        if not bool((lens == self.T).all()):
+            raise NotImplementedError("sharded epochs need full-length trajectories (ErgodicEnv)")
+        self.n_local = self.nt * self.T
+        self.N = self.n_local * self.world
+        self.R0 = self.rank * self.n_local
+        off = torch.arange(self.nt + 1, dtype=torch.int64) * self.T
+        self.offsets = off.to(self.dev)
+        nf = states.shape[-1]
+        self.states_flat = states[:, : self.T].reshape(self.n_local, nf).contiguous()
+        self.actions_flat = actions.reshape(self.n_local, -1).contiguous()
+        self.next_states = next_states_f32.contiguous()
+        self.k = k
+        self._logp_b = None
+        self._stash = None
+
+    # -- collectives (fixed-order reductions: every rank computes bit-identical values) --------
+    def _gather(self, t):
+        """[world, *t.shape] stack of every rank's t (concatenated-form all_gather_into_tensor)."""
+        shape = tuple(t.shape)
+        flat = t.contiguous().reshape(-1)
+        out = torch.empty(self.world * flat.numel(), dtype=t.dtype, device=t.device)
+        self.dist.all_gather_into_tensor(out, flat, group=self.group)
+        return out.reshape((self.world,) + shape)
+
+    def _sum(self, t):
+        return self._gather(t).sum(0)
+
+    # -- per-epoch setup ------------------------------------------------------------------------
+    def build_knn(self):
+        cand = self._gather(self.next_states).reshape(self.N, -1)
+        self.D, self.I, self.idx32T = self.ops.knn(cand, self.k + 1, query=self.next_states)
+        idx_all = self._gather(self.idx32T[: self.k].contiguous())       # [G, k, n_local]
+        idx_allT = idx_all.permute(1, 0, 2).reshape(self.k, self.N).contiguous()
+        self.csr = self.ops.csr_build(idx_allT, self.k, self.n_local, col_offset=self.R0,
+                                      row_offset=0, nq=self.N)
+        return self.D, self.I
+
+    # -- policy log-probs -----------------------------------------------------------------------
+    def _logp(self, policy):
+        return policy.get_log_p(self.states_flat, self.actions_flat).reshape(self.nt, self.T)
+
+    def behavioral_logp(self, policy):
+        from .algorithms.particles import _param_key
+
+        key = _param_key(policy)
+        if self._logp_b is None or self._logp_b[0] != key:
+            with torch.no_grad():
+                self._logp_b = (key, self._logp(policy).detach())
+        return self._logp_b[1]
+
+    def _logps(self, beh, tgt):
+        from .algorithms.particles import _param_key
+
+        lb = self.behavioral_logp(beh)
+        if tgt is beh:
+            return lb, lb
+        if torch.is_grad_enabled() and self._stash is not None:
+            key, lt = self._stash
+            self._stash = None
+            if key == _param_key(tgt):
+                return lt, lb
+        return self._logp(tgt), lb
+
+    # -- forward pieces -------------------------------------------------------------------------
+    def weights(self, logp_t, logp_b):
+        u, ts, _, _ = self.ops.iw_forward(logp_t.detach(), logp_b.detach(), self.offsets,
+                                          self.n_local, normalize=False)
+        U = self._sum(ts.sum().reshape(1)).reshape(())
+        w_local = self.ops.iw_normalize(u, U)
+        return w_local, self._gather(w_local).reshape(self.N)
+
+    def entropy_sums(self, w_global, k, G, B, ns, eps):
+        out4, _, g = self.ops.entropy_forward(w_global, self.idx32T, self.D, k, ns, G, B, eps,
+                                              n_w=self.N)
+        sums = self._sum(out4[2:4].contiguous())
+        H = -sums[0] + B
+        KL = sums[1] / self.N
+        return H, KL, g
+
+    # -- drop-in equivalents of the module-level functions ------------------------------------
+    def compute_entropy(self, beh, tgt, k, G, B, ns, eps):
+        lt, lb = self._logps(beh, tgt)
+        return _ShardedEntropy.apply(lt, lb, self, k, G, B, ns, eps)
+
+    def compute_kl(self, beh, tgt, k, eps):
+        from .algorithms.particles import _param_key
+
+        lb = self.behavioral_logp(beh)
+        if tgt is beh:
+            lt = lb
+        elif torch.is_grad_enabled() and any(p.requires_grad for p in tgt.parameters()):
+            lt = self._logp(tgt)
+            self._stash = (_param_key(tgt), lt)
+        else:
+            with torch.no_grad():
+                lt = self._logp(tgt)
+        with torch.no_grad():
+            _, wg = self.weights(lt, lb)
+            _, KL, _ = self.entropy_sums(wg, k, 1.0, 0.0, 1.0, eps)
+        kl = KL.clone()
+        numeric_error = bool(torch.isinf(kl) or torch.isnan(kl))
+        return torch.clamp_min(kl, 0.0), numeric_error
+
+    def allreduce_grads(self, params):
+        grads = [p.grad for p in params if p.grad is not None]
+        if not grads:
+            return
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        self.dist.all_reduce(flat, group=self.group)
+        o = 0
+        for g in grads:
+            n = g.numel()
+            g.copy_(flat[o:o + n].view_as(g))
+            o += n
+
+    def policy_update(self, optimizer, beh, tgt, k, G, B, ns, eps):
+        optimizer.zero_grad()
+        loss = -self.compute_entropy(beh, tgt, k, G, B, ns, eps)
+        numeric_error = bool(torch.isinf(loss) or torch.isnan(loss))
+        loss.backward()
+        self.allreduce_grads(list(tgt.parameters()))
+        optimizer.step()
+        return loss, numeric_error
+
+    def off_policy_optimization(self, optimizer, beh, tgt, last_valid, G, B, ns, eps,
+                                kl_threshold, max_off_iters, use_backtracking, backtrack_coeff,
+                                max_backtrack_try, original_lr, on_accept=None):
+        from .algorithms.mepol import off_policy_optimization
+
+        k = self.k
+
+        class _Fns:
+            @staticmethod
+            def policy_update(opt, b, t, *a):
+                return self.policy_update(opt, b, t, k, G, B, ns, eps)
+
+            @staticmethod
+            def compute_kl(b, t, *a):
+                return self.compute_kl(b, t, k, eps)
+
+            @staticmethod
+            def compute_entropy(b, t, *a):
+                return self.compute_entropy(b, t, k, G, B, ns, eps)
+
+        return off_policy_optimization(optimizer, beh, tgt, last_valid, None, None, self.nt, None,
+                                       None, None, k, G, B, ns, eps, kl_threshold, max_off_iters,
+                                       use_backtracking, backtrack_coeff, max_backtrack_try,
+                                       original_lr, on_accept, fns=_Fns)
+
+
+class _ShardedEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logp_t, logp_b, ep, k, G, B, ns, eps):
+        w_local, w_global = ep.weights(logp_t, logp_b)
+        H, _, g = ep.entropy_sums(w_global, k, G, B, ns, eps)
+        ctx.ep = ep
+        ctx.save_for_backward(w_local, g)
+        return H.clone()
+
+    @staticmethod
+    def backward(ctx, grad_H):
+        ep = ctx.ep
+        w_local, g = ctx.saved_tensors
+        g_global = ep._gather(g).reshape(ep.N)
+        off, rows = ep.csr
+        gamma, partials, nparts = ep.ops.entropy_gamma(g_global, w_local, off, rows)
+        S = ep._sum(partials[:nparts].sum().reshape(1)).reshape(())
+        gH = grad_H.reshape(()).to(torch.float64).contiguous()
+        grad = ep.ops.entropy_reverse_scan(gamma, w_local, partials, nparts, ep.offsets, ep.nt,
+                                           ep.T, gH, S_ext=S)
+        return grad, None, None, None, None, None, None, None
