@@ -101,6 +101,20 @@ int mepol_entropy_reverse_scan(const double* gamma, const double* w, const doubl
                                int64_t num_traj, int64_t T_stride, const double* grad_H,
                                double* grad_logp, void* stream);
 
+/* ---- Gaussian policy head (GaussianPolicy.get_log_p, src/policy.py:43-51) ----------------
+ * Fused mean layer + log-probability with the last hidden ReLU folded in: z [n, hidden] is the
+ * last hidden layer's PRE-activation; Wm [a_dim, hidden], bm/log_std [a_dim]; act [n, a_dim].
+ * Forward writes mu [n, a_dim] and logp [n].  Backward (grad_logp [n]) writes dz [n, hidden]
+ * (nullable), dWm, dbm, dlog_std.  Limits: hidden <= 512, a_dim <= 8. */
+int mepol_head_forward(const double* z, int64_t n, int hidden, const double* Wm, const double* bm,
+                       const double* log_std, const double* act, int a_dim, double* mu_out,
+                       double* logp_out, void* stream);
+int mepol_head_workspace_size(int64_t n, int hidden, int a_dim, size_t* bytes);
+int mepol_head_backward(const double* grad_logp, const double* z, int64_t n, int hidden,
+                        const double* Wm, const double* log_std, const double* act,
+                        const double* mu, int a_dim, double* dz, double* dWm, double* dbm,
+                        double* dlog_std, void* workspace, size_t workspace_bytes, void* stream);
+
 /* ---- environments -------------------------------------------------------------------------
  * Replace MountainCarContinuous.step (src/envs/mountain_car_wall.py:13-45) and
  * GridWorldContinuous.step (src/envs/gridworld_continuous.py:128-154), batched. */

@@ -1,0 +1,269 @@
+// Fused Gaussian policy head: mean layer + log-probability (GaussianPolicy.get_log_p,
+// src/policy.py:43-51) and its backward, with the last hidden layer's ReLU folded in.
+//
+// forward : h = relu(z);  mu = h Wm^T + bm;  sigma = exp(log_std) + 1e-7
+//           logp_i = sum_a -0.5 (log 2pi + 2 log_std_a + (act_ia - mu_ia)^2 / sigma_a^2)
+// backward: dmu_ia = g_i (act_ia - mu_ia) / sigma_a^2
+//           dlog_std_a = sum_i g_i (-1 + (act_ia - mu_ia)^2 exp(log_std_a) / sigma_a^3)
+//           dbm_a = sum_i dmu_ia ;  dWm_ac = sum_i dmu_ia h_ic
+//           dz_ic = (sum_a dmu_ia Wm_ac) [z_ic > 0]        (ReLU backward fused)
+// One wave per row: z rows are read once, coalesced (64 lanes x 8 B); Wm stays in LDS.  This
+// replaces the PyTorch sequence mean-GEMM, 6 elementwise kernels and a reduction in the forward,
+// and dX-GEMM, dW-GEMM, threshold_backward and the elementwise chain in the backward: the head
+// is HBM-bound (one pass over z forward; z read + dz written backward).
+// Reductions over rows go through per-block partials summed in a fixed order (deterministic).
+#include "common.hpp"
+
+#include <algorithm>
+
+namespace mepol {
+namespace head {
+
+constexpr int kMaxA = 8;      // fused path: action_dim <= 8 (MountainCar 1, GridWorld 2, Ant 8)
+constexpr int kMaxCols = 8;   // columns per lane: hidden <= 512
+constexpr double kLog2Pi = 1.8378770664093453;
+constexpr double kStdEps = 1e-7;
+
+template <int AP>
+__global__ __launch_bounds__(256) void head_fwd_kernel(
+    const double* __restrict__ z, int64_t N, int H, const double* __restrict__ Wm,
+    const double* __restrict__ bm, const double* __restrict__ log_std,
+    const double* __restrict__ act, int A, double* __restrict__ mu_out,
+    double* __restrict__ logp_out) {
+  extern __shared__ __attribute__((aligned(16))) double sW[];  // [A][H]
+  for (int e = threadIdx.x; e < A * H; e += blockDim.x) sW[e] = Wm[e];
+  __syncthreads();
+  const int l = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  double sig2 = 1.0, cst = 0.0, bmv = 0.0;
+  if (l < A) {
+    const double s = exp(log_std[l]) + kStdEps;
+    sig2 = s * s;
+    cst = kLog2Pi + 2.0 * log_std[l];
+    bmv = bm[l];
+  }
+  for (int64_t i = wave; i < N; i += nwaves) {
+    double acc[AP];
+#pragma unroll
+    for (int a = 0; a < AP; ++a) acc[a] = 0.0;
+    const double* zr = z + i * H;
+    for (int c = l; c < H; c += 64) {
+      const double x = fmax(zr[c], 0.0);
+#pragma unroll
+      for (int a = 0; a < AP; ++a)
+        if (a < A) acc[a] += x * sW[a * H + c];
+    }
+    // all-lane sums of the A accumulators; lane a keeps mu_a
+    double mine = 0.0;
+#pragma unroll
+    for (int a = 0; a < AP; ++a) {
+      if (a < A) {
+        const double v = wave_sum(acc[a]);
+        if (l == a) mine = v;
+      }
+    }
+    double term = 0.0;
+    if (l < A) {
+      const double m = mine + bmv;
+      mu_out[i * A + l] = m;
+      const double d = act[i * A + l] - m;
+      term = -0.5 * (cst + d * d / sig2);
+    }
+    const double lp = wave_sum(term);
+    if (l == 0) logp_out[i] = lp;
+  }
+}
+
+// Per-block partials: pdW [nblocks][A][H], pdb [nblocks][A], pdls [nblocks][A].
+template <int AP, int NC>
+__global__ __launch_bounds__(256) void head_bwd_kernel(
+    const double* __restrict__ gl, const double* __restrict__ z, int64_t N, int H,
+    const double* __restrict__ Wm, const double* __restrict__ log_std,
+    const double* __restrict__ act, const double* __restrict__ mu, int A,
+    double* __restrict__ dz, double* __restrict__ pdW, double* __restrict__ pdb,
+    double* __restrict__ pdls) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* sW = sm;                 // [A][H]
+  double* sRed = sm + A * H;       // [A][H] block accumulator (waves add in order 0..3)
+  for (int e = threadIdx.x; e < A * H; e += blockDim.x) sW[e] = Wm[e];
+  __syncthreads();
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  double isig2 = 0.0, es3 = 0.0;
+  if (l < A) {
+    const double e = exp(log_std[l]);
+    const double s = e + kStdEps;
+    isig2 = 1.0 / (s * s);
+    es3 = e / (s * s * s);
+  }
+  double accW[NC][AP];
+#pragma unroll
+  for (int j = 0; j < NC; ++j)
+#pragma unroll
+    for (int a = 0; a < AP; ++a) accW[j][a] = 0.0;
+  double accb = 0.0, accls = 0.0;
+  for (int64_t i = wave; i < N; i += nwaves) {
+    const double g = gl[i];
+    double dmu = 0.0;
+    if (l < A) {
+      const double d = act[i * A + l] - mu[i * A + l];
+      dmu = g * d * isig2;
+      accb += dmu;
+      accls += g * (-1.0 + d * d * es3);
+    }
+    double dm[AP];
+#pragma unroll
+    for (int a = 0; a < AP; ++a) dm[a] = (a < A) ? __shfl(dmu, a, kWave) : 0.0;
+    const double* zr = z + i * H;
+    double* dzr = dz ? dz + i * H : nullptr;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int c = l + 64 * j;
+      if (c < H) {
+        const double zz = zr[c];
+        const double x = fmax(zz, 0.0);
+        double dh = 0.0;
+#pragma unroll
+        for (int a = 0; a < AP; ++a)
+          if (a < A) {
+            dh += dm[a] * sW[a * H + c];
+            accW[j][a] += dm[a] * x;
+          }
+        if (dzr) dzr[c] = (zz > 0.0) ? dh : 0.0;
+      }
+    }
+  }
+  // block reduction of the dW accumulators through LDS, fixed order (waves 0..3)
+  __shared__ double sb[4][kMaxA], sls[4][kMaxA];
+  if (l < A) {
+    sb[w][l] = accb;
+    sls[w][l] = accls;
+  }
+  for (int ww = 0; ww < 4; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const int c = l + 64 * j;
+        if (c < H)
+#pragma unroll
+          for (int a = 0; a < AP; ++a)
+            if (a < A) sRed[a * H + c] = (ww == 0 ? 0.0 : sRed[a * H + c]) + accW[j][a];
+      }
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < A * H; e += blockDim.x) pdW[(int64_t)blockIdx.x * A * H + e] = sRed[e];
+  if (threadIdx.x < A) {
+    const int a = threadIdx.x;
+    pdb[blockIdx.x * A + a] = sb[0][a] + sb[1][a] + sb[2][a] + sb[3][a];
+    pdls[blockIdx.x * A + a] = sls[0][a] + sls[1][a] + sls[2][a] + sls[3][a];
+  }
+}
+
+// out[e] = sum_b part[b][e], fixed order; one thread per element.
+__global__ void reduce_partials_kernel(const double* __restrict__ part, int nblocks, int64_t m,
+                                       double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= m) return;
+  double s = 0.0;
+  for (int b = 0; b < nblocks; ++b) s += part[(int64_t)b * m + e];
+  out[e] = s;
+}
+
+static int grid_for(int64_t N) {
+  const int64_t waves = (N + 7) / 8;  // ~8 rows per wave minimum
+  return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (waves + 3) / 4));
+}
+
+}  // namespace head
+}  // namespace mepol
+
+using namespace mepol;
+using namespace mepol::head;
+
+extern "C" int mepol_head_forward(const double* z, int64_t n, int hidden, const double* Wm,
+                                  const double* bm, const double* log_std, const double* act,
+                                  int a_dim, double* mu_out, double* logp_out, void* stream) {
+  if (n < 0 || hidden <= 0 || hidden > 64 * kMaxCols || a_dim <= 0 || a_dim > kMaxA || !z ||
+      !Wm || !bm || !log_std || !act || !mu_out || !logp_out) {
+    set_error("mepol_head_forward: bad arguments (hidden <= 512, action_dim <= 8)");
+    return kErrBadArg;
+  }
+  if (n == 0) return 0;
+  const size_t lds = (size_t)a_dim * hidden * sizeof(double);
+  dim3 g(grid_for(n));
+  hipStream_t st = (hipStream_t)stream;
+  if (a_dim <= 1)
+    hipLaunchKernelGGL(head_fwd_kernel<1>, g, dim3(256), lds, st, z, n, hidden, Wm, bm, log_std,
+                       act, a_dim, mu_out, logp_out);
+  else if (a_dim <= 2)
+    hipLaunchKernelGGL(head_fwd_kernel<2>, g, dim3(256), lds, st, z, n, hidden, Wm, bm, log_std,
+                       act, a_dim, mu_out, logp_out);
+  else if (a_dim <= 4)
+    hipLaunchKernelGGL(head_fwd_kernel<4>, g, dim3(256), lds, st, z, n, hidden, Wm, bm, log_std,
+                       act, a_dim, mu_out, logp_out);
+  else
+    hipLaunchKernelGGL(head_fwd_kernel<8>, g, dim3(256), lds, st, z, n, hidden, Wm, bm, log_std,
+                       act, a_dim, mu_out, logp_out);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mepol_head_workspace_size(int64_t n, int hidden, int a_dim, size_t* bytes) {
+  if (!bytes || hidden <= 0 || a_dim <= 0) return kErrBadArg;
+  const int nb = grid_for(std::max<int64_t>(n, 1));
+  *bytes = (size_t)nb * a_dim * (hidden + 2) * sizeof(double);
+  return 0;
+}
+
+// dz [n, hidden] (nullable: skip the input gradient), dWm [a_dim, hidden], dbm [a_dim],
+// dlog_std [a_dim] are written (not accumulated).
+extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int64_t n, int hidden,
+                                   const double* Wm, const double* log_std, const double* act,
+                                   const double* mu, int a_dim, double* dz, double* dWm,
+                                   double* dbm, double* dlog_std, void* workspace,
+                                   size_t workspace_bytes, void* stream) {
+  if (n <= 0 || hidden <= 0 || hidden > 64 * kMaxCols || a_dim <= 0 || a_dim > kMaxA ||
+      !grad_logp || !z || !Wm || !log_std || !act || !mu || !dWm || !dbm || !dlog_std ||
+      !workspace) {
+    set_error("mepol_head_backward: bad arguments");
+    return kErrBadArg;
+  }
+  const int nb = grid_for(n);
+  const size_t need = (size_t)nb * a_dim * (hidden + 2) * sizeof(double);
+  if (workspace_bytes < need) {
+    set_error("mepol_head_backward: workspace %zu < %zu", workspace_bytes, need);
+    return kErrWorkspace;
+  }
+  const size_t lds = (size_t)2 * a_dim * hidden * sizeof(double);
+  hipStream_t st = (hipStream_t)stream;
+  double* pdW = (double*)workspace;
+  double* pdb = pdW + (size_t)nb * a_dim * hidden;
+  double* pdls = pdb + (size_t)nb * a_dim;
+  const int nc = (hidden + 63) / 64;
+  const int ap = a_dim <= 1 ? 1 : a_dim <= 2 ? 2 : a_dim <= 4 ? 4 : 8;
+  dim3 g(nb);
+#define MEPOL_HEAD_BWD(AP_, NC_)                                                                  \
+  if (ap == AP_ && nc == NC_)                                                                     \
+    hipLaunchKernelGGL((head_bwd_kernel<AP_, NC_>), g, dim3(256), lds, st, grad_logp, z, n, hidden, \
+                       Wm, log_std, act, mu, a_dim, dz, pdW, pdb, pdls);
+#define MEPOL_HEAD_BWD_A(AP_) \
+  MEPOL_HEAD_BWD(AP_, 1) MEPOL_HEAD_BWD(AP_, 2) MEPOL_HEAD_BWD(AP_, 3) MEPOL_HEAD_BWD(AP_, 4) \
+  MEPOL_HEAD_BWD(AP_, 5) MEPOL_HEAD_BWD(AP_, 6) MEPOL_HEAD_BWD(AP_, 7) MEPOL_HEAD_BWD(AP_, 8)
+  MEPOL_HEAD_BWD_A(1) MEPOL_HEAD_BWD_A(2) MEPOL_HEAD_BWD_A(4) MEPOL_HEAD_BWD_A(8)
+#undef MEPOL_HEAD_BWD_A
+#undef MEPOL_HEAD_BWD
+  MEPOL_CHECK_LAUNCH();
+  const int64_t m = (int64_t)a_dim * hidden;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st,
+                     pdW, nb, m, dWm);
+  MEPOL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(64), 0, st, pdb, nb, (int64_t)a_dim, dbm);
+  MEPOL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(64), 0, st, pdls, nb, (int64_t)a_dim,
+                     dlog_std);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}

@@ -185,6 +185,35 @@ def entropy_reverse_scan(gamma, w, partials, nparts, offsets, nt, T_stride, grad
     return grad
 
 
+def head_forward(z, Wm, bm, log_std, act):
+    """Fused Gaussian head: returns (mu [n, a], logp [n]) from the last PRE-activation z."""
+    n, h = z.shape
+    a = Wm.shape[0]
+    mu = torch.empty((n, a), dtype=torch.float64, device=z.device)
+    logp = torch.empty(n, dtype=torch.float64, device=z.device)
+    call("mepol_head_forward", ptr(z), n, h, ptr(Wm), ptr(bm), ptr(log_std), ptr(act), a, ptr(mu),
+         ptr(logp), _stream())
+    return mu, logp
+
+
+def head_backward(grad_logp, z, Wm, log_std, act, mu, need_dz=True):
+    import ctypes
+
+    n, h = z.shape
+    a = Wm.shape[0]
+    dev = z.device
+    nbytes = ctypes.c_size_t()
+    call("mepol_head_workspace_size", n, h, a, ctypes.byref(nbytes))
+    ws = _workspace(dev, nbytes.value, tag="head")
+    dz = torch.empty_like(z) if need_dz else None
+    dWm = torch.empty_like(Wm)
+    dbm = torch.empty(a, dtype=torch.float64, device=dev)
+    dls = torch.empty(a, dtype=torch.float64, device=dev)
+    call("mepol_head_backward", ptr(grad_logp), ptr(z), n, h, ptr(Wm), ptr(log_std), ptr(act),
+         ptr(mu), a, ptr(dz), ptr(dWm), ptr(dbm), ptr(dls), ptr(ws), ws.numel(), _stream())
+    return dz, dWm, dbm, dls
+
+
 def step_mountaincar(state, action):
     """In-place batched MountainCar step: state f64 [n,2], action f64 [n, a>=1]."""
     _require_device(state, action)

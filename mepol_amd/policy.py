@@ -55,6 +55,28 @@ class _Linear(torch.autograd.Function):
         return gx, gw, gb
 
 
+class _HeadLogp(torch.autograd.Function):
+    """log p(a | s) from the last hidden PRE-activation z via the fused HIP head (csrc/head.hip):
+    relu, mean layer, Gaussian log-density and their backward in one pass each."""
+
+    @staticmethod
+    def forward(ctx, z, w_mean, b_mean, log_std, actions):
+        from . import ops
+
+        mu, logp = ops.head_forward(z, w_mean, b_mean, log_std, actions)
+        ctx.save_for_backward(z, w_mean, log_std, actions, mu)
+        return logp
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import ops
+
+        z, w_mean, log_std, actions, mu = ctx.saved_tensors
+        dz, dw, db, dls = ops.head_backward(g.contiguous(), z, w_mean, log_std, actions, mu,
+                                            need_dz=ctx.needs_input_grad[0])
+        return dz, dw, db, dls, None
+
+
 def _apply_linear(layer, x):
     if x.dim() == 2 and x.shape[0] >= SPLITK_MIN_ROWS and torch.is_grad_enabled():
         return _Linear.apply(x, layer.weight, layer.bias)
@@ -94,8 +116,22 @@ class GaussianPolicy(nn.Module):
             h = _apply_linear(layer, h) if isinstance(layer, nn.Linear) else layer(h)
         return _apply_linear(self.mean, h)
 
+    def _fused_head_ok(self, states, actions):
+        return (states.is_cuda and states.dim() == 2 and states.shape[0] >= SPLITK_MIN_ROWS
+                and self.activation is nn.ReLU and self.action_dim <= 8
+                and self.mean.in_features <= 512 and states.dtype == torch.float64
+                and actions.dtype == torch.float64)
+
     def get_log_p(self, states, actions):
         """sum_a -0.5 (log 2pi + 2 log_std + (a - mu)^2 / (exp(log_std) + 1e-7)^2)."""
+        if self._fused_head_ok(states, actions):
+            layers = [m for m in self.net if isinstance(m, nn.Linear)]
+            h = states
+            for layer in layers[:-1]:
+                h = torch.relu(_apply_linear(layer, h))
+            z = _apply_linear(layers[-1], h).contiguous()
+            return _HeadLogp.apply(z, self.mean.weight.contiguous(), self.mean.bias,
+                                   self.log_std, actions.contiguous())
         mu = self.mean_action(states)
         std = torch.exp(self.log_std) + LOG_STD_EPS
         return torch.sum(-0.5 * (self.log_of_two_pi + 2 * self.log_std + (actions - mu) ** 2 / std ** 2),

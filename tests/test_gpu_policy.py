@@ -1,0 +1,33 @@
+"""Fused HIP Gaussian head (csrc/head.hip) == the PyTorch GaussianPolicy.get_log_p math."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nf,hidden,a", [(2, [300, 300], 2), (2, [300, 300], 1), (29, [400, 300], 8),
+                                         (7, [64, 100], 3), (5, [33], 4)])
+def test_fused_head_matches_unfused(cuda, nf, hidden, a):
+    from mepol_amd import policy as P
+
+    torch.manual_seed(0)
+    pol = P.GaussianPolicy(hidden, nf, a, -0.7).cuda()
+    n = 20000
+    assert n >= P.SPLITK_MIN_ROWS
+    s = torch.randn(n, nf, dtype=torch.float64, device="cuda")
+    act = 0.5 * torch.randn(n, a, dtype=torch.float64, device="cuda")
+    coef = torch.randn(n, dtype=torch.float64, device="cuda")
+    assert pol._fused_head_ok(s, act)
+    lp = pol.get_log_p(s, act)
+    (coef * lp).sum().backward()
+    g_fused = {k: v.grad.clone() for k, v in pol.named_parameters()}
+    pol.zero_grad()
+    mu = pol.mean(pol.net(s))  # plain nn.Module path
+    std = torch.exp(pol.log_std) + 1e-7
+    ref = torch.sum(-0.5 * (P.LOG_2PI + 2 * pol.log_std + (act - mu) ** 2 / std ** 2), dim=1)
+    (coef * ref).sum().backward()
+    assert torch.allclose(lp, ref, rtol=1e-12, atol=1e-12)
+    for k, v in pol.named_parameters():
+        assert torch.allclose(g_fused[k], v.grad, rtol=1e-10, atol=1e-12 * v.grad.abs().max()), k
+    with torch.no_grad():
+        assert torch.allclose(pol.get_log_p(s, act), ref, rtol=1e-12, atol=1e-12)
