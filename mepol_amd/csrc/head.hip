@@ -24,54 +24,86 @@ constexpr int kMaxCols = 8;   // columns per lane: hidden <= 512
 constexpr double kLog2Pi = 1.8378770664093453;
 constexpr double kStdEps = 1e-7;
 
+// Reduce-scatter of AP per-lane partial sums across the wave: log2(AP) halving exchanges, then
+// a butterfly over the remaining lanes.  Afterwards lane l holds the full sum for
+// a = owner(l) (bit-reversed lane bits 5..), every lane of a group of 64/AP holds the same value.
+template <int AP>
+__device__ __forceinline__ double reduce_scatter(double (&v)[AP], int l, int& a_out) {
+  double cur[AP];
+#pragma unroll
+  for (int a = 0; a < AP; ++a) cur[a] = v[a];
+  int a_idx = 0;
+  int len = AP;
+  int bit = 32;
+#pragma unroll
+  for (int step = AP; step > 1; step >>= 1) {
+    const bool upper = (l & bit) != 0;
+    const int half = len >> 1;
+#pragma unroll
+    for (int a = 0; a < AP / 2; ++a) {
+      if (a < half) {
+        const double send = upper ? cur[a] : cur[a + half];
+        const double keep = upper ? cur[a + half] : cur[a];
+        cur[a] = keep + __shfl_xor(send, bit, kWave);
+      }
+    }
+    a_idx = a_idx * 2 + (upper ? 1 : 0);
+    len = half;
+    bit >>= 1;
+  }
+  double x = cur[0];
+  for (; bit >= 1; bit >>= 1) x += __shfl_xor(x, bit, kWave);
+  a_out = a_idx;
+  return x;
+}
+
 template <int AP>
 __global__ __launch_bounds__(256) void head_fwd_kernel(
     const double* __restrict__ z, int64_t N, int H, const double* __restrict__ Wm,
     const double* __restrict__ bm, const double* __restrict__ log_std,
     const double* __restrict__ act, int A, double* __restrict__ mu_out,
     double* __restrict__ logp_out) {
-  extern __shared__ __attribute__((aligned(16))) double sW[];  // [A][H]
-  for (int e = threadIdx.x; e < A * H; e += blockDim.x) sW[e] = Wm[e];
+  extern __shared__ __attribute__((aligned(16))) double sW[];  // [AP][H], rows >= A zero
+  for (int e = threadIdx.x; e < AP * H; e += blockDim.x) sW[e] = (e < A * H) ? Wm[e] : 0.0;
   __syncthreads();
   const int l = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  double sig2 = 1.0, cst = 0.0, bmv = 0.0;
-  if (l < A) {
-    const double s = exp(log_std[l]) + kStdEps;
-    sig2 = s * s;
-    cst = kLog2Pi + 2.0 * log_std[l];
-    bmv = bm[l];
-  }
-  for (int64_t i = wave; i < N; i += nwaves) {
-    double acc[AP];
+  constexpr int R = 2;  // rows in flight per wave
+  for (int64_t i0 = wave * R; i0 < N; i0 += nwaves * R) {
+    double acc[R][AP];
 #pragma unroll
-    for (int a = 0; a < AP; ++a) acc[a] = 0.0;
-    const double* zr = z + i * H;
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int a = 0; a < AP; ++a) acc[r][a] = 0.0;
     for (int c = l; c < H; c += 64) {
-      const double x = fmax(zr[c], 0.0);
+      double x[R];
 #pragma unroll
-      for (int a = 0; a < AP; ++a)
-        if (a < A) acc[a] += x * sW[a * H + c];
-    }
-    // all-lane sums of the A accumulators; lane a keeps mu_a
-    double mine = 0.0;
+      for (int r = 0; r < R; ++r) x[r] = (i0 + r < N) ? fmax(z[(i0 + r) * H + c], 0.0) : 0.0;
 #pragma unroll
-    for (int a = 0; a < AP; ++a) {
-      if (a < A) {
-        const double v = wave_sum(acc[a]);
-        if (l == a) mine = v;
+      for (int a = 0; a < AP; ++a) {
+        const double wv = sW[a * H + c];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r][a] += x[r] * wv;
       }
     }
-    double term = 0.0;
-    if (l < A) {
-      const double m = mine + bmv;
-      mu_out[i * A + l] = m;
-      const double d = act[i * A + l] - m;
-      term = -0.5 * (cst + d * d / sig2);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int64_t i = i0 + r;
+      int a;
+      const double v = reduce_scatter<AP>(acc[r], l, a);
+      double term = 0.0;
+      const bool writer = (l & ((64 / AP) - 1)) == 0;  // one lane per action component
+      if (i < N && a < A) {
+        const double m = v + bm[a];
+        const double s = exp(log_std[a]) + kStdEps;
+        const double d = act[i * A + a] - m;
+        if (writer) mu_out[i * A + a] = m;
+        term = writer ? -0.5 * ((kLog2Pi + 2.0 * log_std[a]) + d * d / (s * s)) : 0.0;
+      }
+      const double lp = wave_sum(term);
+      if (l == 0 && i < N) logp_out[i] = lp;
     }
-    const double lp = wave_sum(term);
-    if (l == 0) logp_out[i] = lp;
   }
 }
 
@@ -98,6 +130,12 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     isig2 = 1.0 / (s * s);
     es3 = e / (s * s * s);
   }
+  double inv_s2[AP];
+#pragma unroll
+  for (int a = 0; a < AP; ++a) {
+    const double e = (a < A) ? exp(log_std[a]) + kStdEps : 1.0;
+    inv_s2[a] = 1.0 / (e * e);
+  }
   double accW[NC][AP];
 #pragma unroll
   for (int j = 0; j < NC; ++j)
@@ -106,16 +144,20 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   double accb = 0.0, accls = 0.0;
   for (int64_t i = wave; i < N; i += nwaves) {
     const double g = gl[i];
-    double dmu = 0.0;
     if (l < A) {
       const double d = act[i * A + l] - mu[i * A + l];
-      dmu = g * d * isig2;
-      accb += dmu;
+      accb += g * d * isig2;
       accls += g * (-1.0 + d * d * es3);
     }
-    double dm[AP];
+    double dm[AP];  // every lane computes all dmu_a (row-uniform loads, no shuffles)
 #pragma unroll
-    for (int a = 0; a < AP; ++a) dm[a] = (a < A) ? __shfl(dmu, a, kWave) : 0.0;
+    for (int a = 0; a < AP; ++a) {
+      if (a < A) {
+        dm[a] = g * (act[i * A + a] - mu[i * A + a]) * inv_s2[a];
+      } else {
+        dm[a] = 0.0;
+      }
+    }
     const double* zr = z + i * H;
     double* dzr = dz ? dz + i * H : nullptr;
 #pragma unroll
@@ -154,27 +196,51 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     }
     __syncthreads();
   }
-  for (int e = threadIdx.x; e < A * H; e += blockDim.x) pdW[(int64_t)blockIdx.x * A * H + e] = sRed[e];
+  const int64_t m = (int64_t)A * H + 2 * A;  // partial record: [dW (A*H) | db (A) | dls (A)]
+  double* rec = pdW + (int64_t)blockIdx.x * m;
+  for (int e = threadIdx.x; e < A * H; e += blockDim.x) rec[e] = sRed[e];
   if (threadIdx.x < A) {
     const int a = threadIdx.x;
-    pdb[blockIdx.x * A + a] = sb[0][a] + sb[1][a] + sb[2][a] + sb[3][a];
-    pdls[blockIdx.x * A + a] = sls[0][a] + sls[1][a] + sls[2][a] + sls[3][a];
+    rec[A * H + a] = sb[0][a] + sb[1][a] + sb[2][a] + sb[3][a];
+    rec[A * H + A + a] = sls[0][a] + sls[1][a] + sls[2][a] + sls[3][a];
   }
 }
 
-// out[e] = sum_b part[b][e], fixed order; one thread per element.
-__global__ void reduce_partials_kernel(const double* __restrict__ part, int nblocks, int64_t m,
-                                       double* __restrict__ out) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= m) return;
+// out = sum_b part[b][:] in a fixed order: 64 elements per block, wave w sums a quarter of the
+// partials, the 4 quarter sums are added in order.  dW goes to dWm, the tail to dbm / dls.
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __restrict__ part,
+                                                              int nblocks, int64_t m, int AH,
+                                                              int A, double* __restrict__ dWm,
+                                                              double* __restrict__ dbm,
+                                                              double* __restrict__ dls) {
+  __shared__ double sh[4][64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + l;
+  const int q = (nblocks + 3) / 4;
+  const int b0 = w * q, b1 = min(nblocks, b0 + q);
   double s = 0.0;
-  for (int b = 0; b < nblocks; ++b) s += part[(int64_t)b * m + e];
-  out[e] = s;
+  if (e < m)
+    for (int b = b0; b < b1; ++b) s += part[(int64_t)b * m + e];
+  sh[w][l] = s;
+  __syncthreads();
+  if (w == 0 && e < m) {
+    const double t = ((sh[0][l] + sh[1][l]) + sh[2][l]) + sh[3][l];
+    if (e < AH)
+      dWm[e] = t;
+    else if (e < AH + A)
+      dbm[e - AH] = t;
+    else
+      dls[e - AH - A] = t;
+  }
 }
 
 static int grid_for(int64_t N) {
-  const int64_t waves = (N + 7) / 8;  // ~8 rows per wave minimum
+  const int64_t waves = (N + 15) / 16;  // >= 16 rows per wave
   return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (waves + 3) / 4));
+}
+static int grid_bwd(int64_t N) {
+  const int64_t waves = (N + 63) / 64;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(256, (waves + 3) / 4));
 }
 
 }  // namespace head
@@ -192,7 +258,8 @@ extern "C" int mepol_head_forward(const double* z, int64_t n, int hidden, const 
     return kErrBadArg;
   }
   if (n == 0) return 0;
-  const size_t lds = (size_t)a_dim * hidden * sizeof(double);
+  const int ap0 = a_dim <= 1 ? 1 : a_dim <= 2 ? 2 : a_dim <= 4 ? 4 : 8;
+  const size_t lds = (size_t)ap0 * hidden * sizeof(double);
   dim3 g(grid_for(n));
   hipStream_t st = (hipStream_t)stream;
   if (a_dim <= 1)
@@ -213,7 +280,7 @@ extern "C" int mepol_head_forward(const double* z, int64_t n, int hidden, const 
 
 extern "C" int mepol_head_workspace_size(int64_t n, int hidden, int a_dim, size_t* bytes) {
   if (!bytes || hidden <= 0 || a_dim <= 0) return kErrBadArg;
-  const int nb = grid_for(std::max<int64_t>(n, 1));
+  const int nb = grid_bwd(std::max<int64_t>(n, 1));
   *bytes = (size_t)nb * a_dim * (hidden + 2) * sizeof(double);
   return 0;
 }
@@ -231,7 +298,7 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
     set_error("mepol_head_backward: bad arguments");
     return kErrBadArg;
   }
-  const int nb = grid_for(n);
+  const int nb = grid_bwd(n);
   const size_t need = (size_t)nb * a_dim * (hidden + 2) * sizeof(double);
   if (workspace_bytes < need) {
     set_error("mepol_head_backward: workspace %zu < %zu", workspace_bytes, need);
@@ -240,8 +307,8 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
   const size_t lds = (size_t)2 * a_dim * hidden * sizeof(double);
   hipStream_t st = (hipStream_t)stream;
   double* pdW = (double*)workspace;
-  double* pdb = pdW + (size_t)nb * a_dim * hidden;
-  double* pdls = pdb + (size_t)nb * a_dim;
+  double* pdb = nullptr;
+  double* pdls = nullptr;
   const int nc = (hidden + 63) / 64;
   const int ap = a_dim <= 1 ? 1 : a_dim <= 2 ? 2 : a_dim <= 4 ? 4 : 8;
   dim3 g(nb);
@@ -256,14 +323,9 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
 #undef MEPOL_HEAD_BWD_A
 #undef MEPOL_HEAD_BWD
   MEPOL_CHECK_LAUNCH();
-  const int64_t m = (int64_t)a_dim * hidden;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st,
-                     pdW, nb, m, dWm);
-  MEPOL_CHECK_LAUNCH();
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(64), 0, st, pdb, nb, (int64_t)a_dim, dbm);
-  MEPOL_CHECK_LAUNCH();
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(64), 0, st, pdls, nb, (int64_t)a_dim,
-                     dlog_std);
+  const int64_t m = (int64_t)a_dim * hidden + 2 * a_dim;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st, pdW,
+                     nb, m, a_dim * hidden, a_dim, dWm, dbm, dlog_std);
   MEPOL_CHECK_LAUNCH();
   return 0;
 }
