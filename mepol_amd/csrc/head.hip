@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
   const int l = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  constexpr int R = 2;  // rows in flight per wave
+  constexpr int R = 4;  // rows in flight per wave
   for (int64_t i0 = wave * R; i0 < N; i0 += nwaves * R) {
     double acc[R][AP];
 #pragma unroll
@@ -142,38 +142,44 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
 #pragma unroll
     for (int a = 0; a < AP; ++a) accW[j][a] = 0.0;
   double accb = 0.0, accls = 0.0;
-  for (int64_t i = wave; i < N; i += nwaves) {
-    const double g = gl[i];
-    if (l < A) {
-      const double d = act[i * A + l] - mu[i * A + l];
-      accb += g * d * isig2;
-      accls += g * (-1.0 + d * d * es3);
-    }
-    double dm[AP];  // every lane computes all dmu_a (row-uniform loads, no shuffles)
+  constexpr int R = 2;  // rows in flight per wave
+  for (int64_t i0 = wave * R; i0 < N; i0 += nwaves * R) {
+    double zz[R][NC];
 #pragma unroll
-    for (int a = 0; a < AP; ++a) {
-      if (a < A) {
-        dm[a] = g * (act[i * A + a] - mu[i * A + a]) * inv_s2[a];
-      } else {
-        dm[a] = 0.0;
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const int c = l + 64 * j;
+        zz[r][j] = (i0 + r < N && c < H) ? z[(i0 + r) * H + c] : 0.0;
       }
-    }
-    const double* zr = z + i * H;
-    double* dzr = dz ? dz + i * H : nullptr;
 #pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      const int c = l + 64 * j;
-      if (c < H) {
-        const double zz = zr[c];
-        const double x = fmax(zz, 0.0);
-        double dh = 0.0;
+    for (int r = 0; r < R; ++r) {
+      const int64_t i = i0 + r;
+      if (i >= N) break;
+      const double g = gl[i];
+      if (l < A) {
+        const double d = act[i * A + l] - mu[i * A + l];
+        accb += g * d * isig2;
+        accls += g * (-1.0 + d * d * es3);
+      }
+      double dm[AP];  // every lane computes all dmu_a (row-uniform loads, no shuffles)
 #pragma unroll
-        for (int a = 0; a < AP; ++a)
-          if (a < A) {
-            dh += dm[a] * sW[a * H + c];
-            accW[j][a] += dm[a] * x;
-          }
-        if (dzr) dzr[c] = (zz > 0.0) ? dh : 0.0;
+      for (int a = 0; a < AP; ++a) dm[a] = (a < A) ? g * (act[i * A + a] - mu[i * A + a]) * inv_s2[a] : 0.0;
+      double* dzr = dz ? dz + i * H : nullptr;
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const int c = l + 64 * j;
+        if (c < H) {
+          const double x = fmax(zz[r][j], 0.0);
+          double dh = 0.0;
+#pragma unroll
+          for (int a = 0; a < AP; ++a)
+            if (a < A) {
+              dh += dm[a] * sW[a * H + c];
+              accW[j][a] += dm[a] * x;
+            }
+          if (dzr) dzr[c] = (zz[r][j] > 0.0) ? dh : 0.0;
+        }
       }
     }
   }
@@ -239,8 +245,8 @@ static int grid_for(int64_t N) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (waves + 3) / 4));
 }
 static int grid_bwd(int64_t N) {
-  const int64_t waves = (N + 63) / 64;
-  return (int)std::max<int64_t>(1, std::min<int64_t>(256, (waves + 3) / 4));
+  const int64_t waves = (N + 31) / 32;  // >= 32 rows per wave
+  return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (waves + 3) / 4));
 }
 
 }  // namespace head
