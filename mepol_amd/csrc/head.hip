@@ -57,158 +57,175 @@ __device__ __forceinline__ double reduce_scatter(double (&v)[AP], int l, int& a_
   return x;
 }
 
-template <int AP>
+// One wave per row, lane l owns columns c = l + 64 j (j < NC); the lane's slice of Wm lives in
+// VGPRs (NC x AP doubles), rows are software-pipelined (next row's z loads issued before the
+// current row's math), so the kernel streams z at HBM rate with no LDS traffic.
+template <int AP, int NC>
 __global__ __launch_bounds__(256) void head_fwd_kernel(
     const double* __restrict__ z, int64_t N, int H, const double* __restrict__ Wm,
     const double* __restrict__ bm, const double* __restrict__ log_std,
     const double* __restrict__ act, int A, double* __restrict__ mu_out,
     double* __restrict__ logp_out) {
-  extern __shared__ __attribute__((aligned(16))) double sW[];  // [AP][H], rows >= A zero
-  for (int e = threadIdx.x; e < AP * H; e += blockDim.x) sW[e] = (e < A * H) ? Wm[e] : 0.0;
-  __syncthreads();
+  __shared__ double sW[NC * 64 * AP];  // [j][a][lane]: lane-contiguous, conflict-free
   const int l = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  constexpr int R = 4;  // rows in flight per wave
-  for (int64_t i0 = wave * R; i0 < N; i0 += nwaves * R) {
-    double acc[R][AP];
+  for (int e = threadIdx.x; e < NC * 64 * AP; e += blockDim.x) {
+    const int ll = e & 63, a = (e >> 6) % AP, j = (e >> 6) / AP;
+    const int c = ll + 64 * j;
+    sW[e] = (c < H && a < A) ? Wm[a * H + c] : 0.0;
+  }
+  __syncthreads();
+  double zn[NC];
+  auto load_row = [&](int64_t i) {
 #pragma unroll
-    for (int r = 0; r < R; ++r)
-#pragma unroll
-      for (int a = 0; a < AP; ++a) acc[r][a] = 0.0;
-    for (int c = l; c < H; c += 64) {
-      double x[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) x[r] = (i0 + r < N) ? fmax(z[(i0 + r) * H + c], 0.0) : 0.0;
-#pragma unroll
-      for (int a = 0; a < AP; ++a) {
-        const double wv = sW[a * H + c];
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r][a] += x[r] * wv;
-      }
+    for (int j = 0; j < NC; ++j) {
+      const int c = l + 64 * j;
+      zn[j] = (i < N && c < H) ? z[i * H + c] : 0.0;
     }
+  };
+  load_row(wave);
+  for (int64_t i = wave; i < N; i += nwaves) {
+    double zc[NC];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int64_t i = i0 + r;
-      int a;
-      const double v = reduce_scatter<AP>(acc[r], l, a);
-      double term = 0.0;
-      const bool writer = (l & ((64 / AP) - 1)) == 0;  // one lane per action component
-      if (i < N && a < A) {
-        const double m = v + bm[a];
-        const double s = exp(log_std[a]) + kStdEps;
-        const double d = act[i * A + a] - m;
-        if (writer) mu_out[i * A + a] = m;
-        term = writer ? -0.5 * ((kLog2Pi + 2.0 * log_std[a]) + d * d / (s * s)) : 0.0;
-      }
-      const double lp = wave_sum(term);
-      if (l == 0 && i < N) logp_out[i] = lp;
+    for (int j = 0; j < NC; ++j) zc[j] = zn[j];
+    load_row(i + nwaves);
+    double acc[AP];
+#pragma unroll
+    for (int a = 0; a < AP; ++a) acc[a] = 0.0;
+    int lo = l;
+    asm volatile("" : "+v"(lo));  // keep the Wm LDS reads in the loop (no hoist into VGPRs)
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const double x = fmax(zc[j], 0.0);
+#pragma unroll
+      for (int a = 0; a < AP; ++a) acc[a] += x * sW[(j * AP + a) * 64 + lo];
     }
+    int a;
+    const double v = reduce_scatter<AP>(acc, l, a);
+    double term = 0.0;
+    const bool writer = (l & ((64 / AP) - 1)) == 0;  // one lane per action component
+    if (a < A && writer) {
+      const double m = v + bm[a];
+      const double sd = exp(log_std[a]) + kStdEps;
+      const double d = act[i * A + a] - m;
+      mu_out[i * A + a] = m;
+      term = -0.5 * ((kLog2Pi + 2.0 * log_std[a]) + d * d / (sd * sd));
+    }
+    const double lp = wave_sum(term);
+    if (l == 0) logp_out[i] = lp;
   }
 }
 
-// Per-block partials: pdW [nblocks][A][H], pdb [nblocks][A], pdls [nblocks][A].
+// Per-block partial records [dW (A*H) | db (A) | dls (A)], reduced by reduce_partials_kernel.
 template <int AP, int NC>
 __global__ __launch_bounds__(256) void head_bwd_kernel(
     const double* __restrict__ gl, const double* __restrict__ z, int64_t N, int H,
     const double* __restrict__ Wm, const double* __restrict__ log_std,
     const double* __restrict__ act, const double* __restrict__ mu, int A,
-    double* __restrict__ dz, double* __restrict__ pdW, double* __restrict__ pdb,
-    double* __restrict__ pdls) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  double* sW = sm;                 // [A][H]
-  double* sRed = sm + A * H;       // [A][H] block accumulator (waves add in order 0..3)
-  for (int e = threadIdx.x; e < A * H; e += blockDim.x) sW[e] = Wm[e];
-  __syncthreads();
+    double* __restrict__ dz, double* __restrict__ part) {
+  __shared__ double sW[NC * 64 * AP];   // [j][a][lane]
+  __shared__ double sRed[AP * 64 * NC];  // block accumulator, waves add in order 0..3
+  __shared__ double sb[4][AP], sls[4][AP];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  double isig2 = 0.0, es3 = 0.0;
+  for (int e = threadIdx.x; e < NC * 64 * AP; e += blockDim.x) {
+    const int ll = e & 63, a = (e >> 6) % AP, j = (e >> 6) / AP;
+    const int c = ll + 64 * j;
+    sW[e] = (c < H && a < A) ? Wm[a * H + c] : 0.0;
+  }
+  __syncthreads();
+  __shared__ double sInv[AP];
+  if (threadIdx.x < AP) {
+    const int a = threadIdx.x;
+    const double e = (a < A) ? exp(log_std[a]) : 1.0;
+    const double sd = e + kStdEps;
+    sInv[a] = 1.0 / (sd * sd);
+  }
+  double es3 = 0.0;  // lane a (< A) owns component a of db / dlog_std
   if (l < A) {
     const double e = exp(log_std[l]);
-    const double s = e + kStdEps;
-    isig2 = 1.0 / (s * s);
-    es3 = e / (s * s * s);
+    const double sd = e + kStdEps;
+    es3 = e / (sd * sd * sd);
   }
-  double inv_s2[AP];
-#pragma unroll
-  for (int a = 0; a < AP; ++a) {
-    const double e = (a < A) ? exp(log_std[a]) + kStdEps : 1.0;
-    inv_s2[a] = 1.0 / (e * e);
-  }
+  __syncthreads();
   double accW[NC][AP];
 #pragma unroll
   for (int j = 0; j < NC; ++j)
 #pragma unroll
     for (int a = 0; a < AP; ++a) accW[j][a] = 0.0;
-  double accb = 0.0, accls = 0.0;
-  constexpr int R = 2;  // rows in flight per wave
-  for (int64_t i0 = wave * R; i0 < N; i0 += nwaves * R) {
-    double zz[R][NC];
+  double accb = 0.0, accls = 0.0;  // lane a (< A) accumulates component a
+  double zn[NC];
+  auto load_row = [&](int64_t i) {
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+    for (int j = 0; j < NC; ++j) {
+      const int c = l + 64 * j;
+      zn[j] = (i < N && c < H) ? z[i * H + c] : 0.0;
+    }
+  };
+  load_row(wave);
+  for (int64_t i = wave; i < N; i += nwaves) {
+    double zc[NC];
 #pragma unroll
-      for (int j = 0; j < NC; ++j) {
-        const int c = l + 64 * j;
-        zz[r][j] = (i0 + r < N && c < H) ? z[(i0 + r) * H + c] : 0.0;
-      }
+    for (int j = 0; j < NC; ++j) zc[j] = zn[j];
+    load_row(i + nwaves);
+    const double g = gl[i];
+    double dm[AP];  // every lane computes all dmu_a from row-uniform loads
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int64_t i = i0 + r;
-      if (i >= N) break;
-      const double g = gl[i];
-      if (l < A) {
-        const double d = act[i * A + l] - mu[i * A + l];
-        accb += g * d * isig2;
+    for (int a = 0; a < AP; ++a) {
+      const double d = (a < A) ? act[i * A + a] - mu[i * A + a] : 0.0;
+      dm[a] = g * d * sInv[a];
+      if (a == l) {
+        accb += dm[a];
         accls += g * (-1.0 + d * d * es3);
       }
-      double dm[AP];  // every lane computes all dmu_a (row-uniform loads, no shuffles)
+    }
+    double* dzr = dz ? dz + i * H : nullptr;
+    int lo = l;
+    asm volatile("" : "+v"(lo));  // keep the Wm LDS reads in the loop (no hoist into VGPRs)
 #pragma unroll
-      for (int a = 0; a < AP; ++a) dm[a] = (a < A) ? g * (act[i * A + a] - mu[i * A + a]) * inv_s2[a] : 0.0;
-      double* dzr = dz ? dz + i * H : nullptr;
+    for (int j = 0; j < NC; ++j) {
+      const int c = l + 64 * j;
+      const double x = fmax(zc[j], 0.0);
+      double dh = 0.0;
 #pragma unroll
-      for (int j = 0; j < NC; ++j) {
-        const int c = l + 64 * j;
-        if (c < H) {
-          const double x = fmax(zz[r][j], 0.0);
-          double dh = 0.0;
-#pragma unroll
-          for (int a = 0; a < AP; ++a)
-            if (a < A) {
-              dh += dm[a] * sW[a * H + c];
-              accW[j][a] += dm[a] * x;
-            }
-          if (dzr) dzr[c] = (zz[r][j] > 0.0) ? dh : 0.0;
-        }
+      for (int a = 0; a < AP; ++a) {
+        dh += dm[a] * sW[(j * AP + a) * 64 + lo];
+        accW[j][a] += dm[a] * x;
       }
+      if (dzr && c < H) dzr[c] = (zc[j] > 0.0) ? dh : 0.0;
     }
   }
-  // block reduction of the dW accumulators through LDS, fixed order (waves 0..3)
-  __shared__ double sb[4][kMaxA], sls[4][kMaxA];
-  if (l < A) {
+  // block reduction in a fixed order (waves 0..3), then one record per block
+  if (l < AP) {
     sb[w][l] = accb;
     sls[w][l] = accls;
   }
   for (int ww = 0; ww < 4; ++ww) {
     if (w == ww) {
 #pragma unroll
-      for (int j = 0; j < NC; ++j) {
-        const int c = l + 64 * j;
-        if (c < H)
+      for (int j = 0; j < NC; ++j)
 #pragma unroll
-          for (int a = 0; a < AP; ++a)
-            if (a < A) sRed[a * H + c] = (ww == 0 ? 0.0 : sRed[a * H + c]) + accW[j][a];
-      }
+        for (int a = 0; a < AP; ++a) {
+          const int idx = (a * NC + j) * 64 + l;
+          sRed[idx] = (ww == 0 ? 0.0 : sRed[idx]) + accW[j][a];
+        }
     }
     __syncthreads();
   }
-  const int64_t m = (int64_t)A * H + 2 * A;  // partial record: [dW (A*H) | db (A) | dls (A)]
-  double* rec = pdW + (int64_t)blockIdx.x * m;
-  for (int e = threadIdx.x; e < A * H; e += blockDim.x) rec[e] = sRed[e];
+  const int64_t m = (int64_t)A * H + 2 * A;
+  double* rec = part + (int64_t)blockIdx.x * m;
+  for (int e = threadIdx.x; e < A * H; e += blockDim.x) {
+    const int a = e / H, c = e % H;
+    const int j = c >> 6, ll = c & 63;
+    const int idx = (a * NC + j) * 64 + ll;
+    rec[e] = sRed[idx];
+  }
   if (threadIdx.x < A) {
     const int a = threadIdx.x;
-    rec[A * H + a] = sb[0][a] + sb[1][a] + sb[2][a] + sb[3][a];
-    rec[A * H + A + a] = sls[0][a] + sls[1][a] + sls[2][a] + sls[3][a];
+    rec[A * H + a] = ((sb[0][a] + sb[1][a]) + sb[2][a]) + sb[3][a];
+    rec[A * H + A + a] = ((sls[0][a] + sls[1][a]) + sls[2][a]) + sls[3][a];
   }
 }
 
@@ -241,12 +258,12 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __re
 }
 
 static int grid_for(int64_t N) {
-  const int64_t waves = (N + 15) / 16;  // >= 16 rows per wave
+  const int64_t waves = (N + 7) / 8;  // >= 8 rows per wave
   return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (waves + 3) / 4));
 }
 static int grid_bwd(int64_t N) {
   const int64_t waves = (N + 31) / 32;  // >= 32 rows per wave
-  return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (waves + 3) / 4));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(512, (waves + 3) / 4));
 }
 
 }  // namespace head
@@ -264,22 +281,20 @@ extern "C" int mepol_head_forward(const double* z, int64_t n, int hidden, const 
     return kErrBadArg;
   }
   if (n == 0) return 0;
-  const int ap0 = a_dim <= 1 ? 1 : a_dim <= 2 ? 2 : a_dim <= 4 ? 4 : 8;
-  const size_t lds = (size_t)ap0 * hidden * sizeof(double);
+  const int ap = a_dim <= 1 ? 1 : a_dim <= 2 ? 2 : a_dim <= 4 ? 4 : 8;
+  const int nc = (hidden + 63) / 64;
   dim3 g(grid_for(n));
   hipStream_t st = (hipStream_t)stream;
-  if (a_dim <= 1)
-    hipLaunchKernelGGL(head_fwd_kernel<1>, g, dim3(256), lds, st, z, n, hidden, Wm, bm, log_std,
-                       act, a_dim, mu_out, logp_out);
-  else if (a_dim <= 2)
-    hipLaunchKernelGGL(head_fwd_kernel<2>, g, dim3(256), lds, st, z, n, hidden, Wm, bm, log_std,
-                       act, a_dim, mu_out, logp_out);
-  else if (a_dim <= 4)
-    hipLaunchKernelGGL(head_fwd_kernel<4>, g, dim3(256), lds, st, z, n, hidden, Wm, bm, log_std,
-                       act, a_dim, mu_out, logp_out);
-  else
-    hipLaunchKernelGGL(head_fwd_kernel<8>, g, dim3(256), lds, st, z, n, hidden, Wm, bm, log_std,
-                       act, a_dim, mu_out, logp_out);
+#define MEPOL_HEAD_FWD(AP_, NC_)                                                                \
+  if (ap == AP_ && nc == NC_)                                                                   \
+    hipLaunchKernelGGL((head_fwd_kernel<AP_, NC_>), g, dim3(256), 0, st, z, n, hidden, Wm, bm,  \
+                       log_std, act, a_dim, mu_out, logp_out);
+#define MEPOL_HEAD_FWD_A(AP_) \
+  MEPOL_HEAD_FWD(AP_, 1) MEPOL_HEAD_FWD(AP_, 2) MEPOL_HEAD_FWD(AP_, 3) MEPOL_HEAD_FWD(AP_, 4) \
+  MEPOL_HEAD_FWD(AP_, 5) MEPOL_HEAD_FWD(AP_, 6) MEPOL_HEAD_FWD(AP_, 7) MEPOL_HEAD_FWD(AP_, 8)
+  MEPOL_HEAD_FWD_A(1) MEPOL_HEAD_FWD_A(2) MEPOL_HEAD_FWD_A(4) MEPOL_HEAD_FWD_A(8)
+#undef MEPOL_HEAD_FWD_A
+#undef MEPOL_HEAD_FWD
   MEPOL_CHECK_LAUNCH();
   return 0;
 }
@@ -310,18 +325,15 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
     set_error("mepol_head_backward: workspace %zu < %zu", workspace_bytes, need);
     return kErrWorkspace;
   }
-  const size_t lds = (size_t)2 * a_dim * hidden * sizeof(double);
   hipStream_t st = (hipStream_t)stream;
   double* pdW = (double*)workspace;
-  double* pdb = nullptr;
-  double* pdls = nullptr;
   const int nc = (hidden + 63) / 64;
   const int ap = a_dim <= 1 ? 1 : a_dim <= 2 ? 2 : a_dim <= 4 ? 4 : 8;
   dim3 g(nb);
 #define MEPOL_HEAD_BWD(AP_, NC_)                                                                  \
   if (ap == AP_ && nc == NC_)                                                                     \
-    hipLaunchKernelGGL((head_bwd_kernel<AP_, NC_>), g, dim3(256), lds, st, grad_logp, z, n, hidden, \
-                       Wm, log_std, act, mu, a_dim, dz, pdW, pdb, pdls);
+    hipLaunchKernelGGL((head_bwd_kernel<AP_, NC_>), g, dim3(256), 0, st, grad_logp, z, n, hidden, \
+                       Wm, log_std, act, mu, a_dim, dz, pdW);
 #define MEPOL_HEAD_BWD_A(AP_) \
   MEPOL_HEAD_BWD(AP_, 1) MEPOL_HEAD_BWD(AP_, 2) MEPOL_HEAD_BWD(AP_, 3) MEPOL_HEAD_BWD(AP_, 4) \
   MEPOL_HEAD_BWD(AP_, 5) MEPOL_HEAD_BWD(AP_, 6) MEPOL_HEAD_BWD(AP_, 7) MEPOL_HEAD_BWD(AP_, 8)
