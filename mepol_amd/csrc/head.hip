@@ -84,8 +84,22 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
       zn[j] = (i < N && c < H) ? z[i * H + c] : 0.0;
     }
   };
-  load_row(wave);
-  for (int64_t i = wave; i < N; i += nwaves) {
+  double bmu[AP], cst[AP], is2[AP];  // wave-uniform constants (scalar registers)
+#pragma unroll
+  for (int a = 0; a < AP; ++a) {
+    const double lsa = (a < A) ? log_std[a] : 0.0;
+    const double sd = exp(lsa) + kStdEps;
+    bmu[a] = (a < A) ? bm[a] : 0.0;
+    cst[a] = kLog2Pi + 2.0 * lsa;
+    is2[a] = 1.0 / (sd * sd);
+  }
+  const int64_t wave_u = __builtin_amdgcn_readfirstlane((int)wave);
+  load_row(wave_u);
+  for (int64_t i = wave_u; i < N; i += nwaves) {
+    // row-uniform scalar loads first, so waiting on them never drains the z prefetch below
+    double av[AP];
+#pragma unroll
+    for (int a = 0; a < AP; ++a) av[a] = (a < A) ? act[i * A + a] : 0.0;
     double zc[NC];
 #pragma unroll
     for (int j = 0; j < NC; ++j) zc[j] = zn[j];
@@ -105,12 +119,20 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
     const double v = reduce_scatter<AP>(acc, l, a);
     double term = 0.0;
     const bool writer = (l & ((64 / AP) - 1)) == 0;  // one lane per action component
+    double b_a = 0.0, c_a = 0.0, i_a = 0.0, x_a = 0.0;
+#pragma unroll
+    for (int q = 0; q < AP; ++q)
+      if (a == q) {
+        b_a = bmu[q];
+        c_a = cst[q];
+        i_a = is2[q];
+        x_a = av[q];
+      }
     if (a < A && writer) {
-      const double m = v + bm[a];
-      const double sd = exp(log_std[a]) + kStdEps;
-      const double d = act[i * A + a] - m;
+      const double m = v + b_a;
+      const double d = x_a - m;
       mu_out[i * A + a] = m;
-      term = -0.5 * ((kLog2Pi + 2.0 * log_std[a]) + d * d / (sd * sd));
+      term = -0.5 * (c_a + d * d * i_a);
     }
     const double lp = wave_sum(term);
     if (l == 0) logp_out[i] = lp;
@@ -164,17 +186,25 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       zn[j] = (i < N && c < H) ? z[i * H + c] : 0.0;
     }
   };
-  load_row(wave);
-  for (int64_t i = wave; i < N; i += nwaves) {
+  const int64_t wave_u = __builtin_amdgcn_readfirstlane((int)wave);
+  load_row(wave_u);
+  for (int64_t i = wave_u; i < N; i += nwaves) {
+    // row-uniform scalar loads first (they do not count against the z prefetch's vmcnt)
+    const double g = gl[i];
+    double av[AP], mv[AP];
+#pragma unroll
+    for (int a = 0; a < AP; ++a) {
+      av[a] = (a < A) ? act[i * A + a] : 0.0;
+      mv[a] = (a < A) ? mu[i * A + a] : 0.0;
+    }
     double zc[NC];
 #pragma unroll
     for (int j = 0; j < NC; ++j) zc[j] = zn[j];
     load_row(i + nwaves);
-    const double g = gl[i];
     double dm[AP];  // every lane computes all dmu_a from row-uniform loads
 #pragma unroll
     for (int a = 0; a < AP; ++a) {
-      const double d = (a < A) ? act[i * A + a] - mu[i * A + a] : 0.0;
+      const double d = av[a] - mv[a];
       dm[a] = g * d * sInv[a];
       if (a == l) {
         accb += dm[a];
