@@ -11,7 +11,10 @@ all: $(LIB)
 
 build/%.o: mepol_amd/csrc/%.hip mepol_amd/csrc/common.hpp include/mepol_amd.h
 	@mkdir -p build
-	$(HIPCC) $(FLAGS) -Iinclude -c $< -o $@
+	$(HIPCC) $(FLAGS) $(FLAGS_$*) -Iinclude -c $< -o $@
+
+# k-NN selection compares finite MFMA outputs: no NaN canonicalisation before v_min
+FLAGS_knn := -fno-honor-nans
 
 $(LIB): $(OBJ)
 	$(HIPCC) $(FLAGS) -shared -o $@ $(OBJ)

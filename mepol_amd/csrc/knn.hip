@@ -30,6 +30,7 @@ namespace mepol {
 namespace knn {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
 
 constexpr float kPadNorm = 1e30f;  // |c|^2 of padding candidates: never selected
 constexpr int kBufCap = 24;        // per-lane LDS insertion buffer (entries)
@@ -151,6 +152,12 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ a
     bq[s] = qvalid ? ((f < d) ? query[q * d + f] : ((f == d) ? 1.f : 0.f)) : 0.f;
   }
 
+  // Retire the B-operand loads here and launder the registers, so no compiler-tracked load is
+  // pending inside the tile loop (otherwise its waitcnt pass drains vmcnt(0) every iteration).
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(bq[s]));
+
   float ld[LIST];
   int li[LIST];
 #pragma unroll
@@ -165,31 +172,44 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ a
   const int64_t t1 = min(nct, t0 + tiles_per_split);
 
   constexpr int NV = KSP / 4;
-  float an[KSP];
-  const float* abase = apack + (int64_t)l * KSP;
-  auto load_tile = [&](int64_t t) {
-    const float4* p = reinterpret_cast<const float4*>(abase + t * 64 * KSP);
+  const f32x4* abase = reinterpret_cast<const f32x4*>(apack + (int64_t)l * KSP);
+  // Two register buffers (ping-pong): tile t+1's loads are in flight while tile t's MFMA chain
+  // runs.  Fragment loads are issued from inline asm so the compiler's waitcnt pass (which
+  // drains to vmcnt(0) at this loop's control-flow joins) does not see them; the waits are
+  // counted by hand: the only vector-memory ops inside the loop are these NV loads per tile.
+  f32x4 A0[NV], A1[NV];
+  auto load = [&](f32x4 (&A)[NV], int64_t t) {
+    const f32x4* p = abase + t * 16 * KSP;  // 64 lanes * KSP floats = 16*KSP f32x4 per tile
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-      const float4 x = p[v];
-      an[4 * v + 0] = x.x;
-      an[4 * v + 1] = x.y;
-      an[4 * v + 2] = x.z;
-      an[4 * v + 3] = x.w;
+      f32x4 x;
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(p + v) : "memory");
+      A[v] = x;
     }
   };
-  if (t0 < t1) load_tile(t0);
-
-#pragma nounroll
-  for (int64_t t = t0; t < t1; ++t) {
-    float a[KSP];
+  auto wait_older = [&](f32x4 (&A)[NV]) {  // all but the NV youngest loads have landed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV) : "memory");
 #pragma unroll
-    for (int v = 0; v < KSP; ++v) a[v] = an[v];
-    if (t + 1 < t1) load_tile(t + 1);
+    for (int v = 0; v < NV; ++v) {
+      f32x4 x = A[v];
+      asm volatile("" : "+v"(x));
+      A[v] = x;
+    }
+  };
+  auto wait_all = [&](f32x4 (&A)[NV]) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      f32x4 x = A[v];
+      asm volatile("" : "+v"(x));
+      A[v] = x;
+    }
+  };
+  auto comp = [](const f32x4 (&A)[NV], int s) -> float { return A[s >> 2][s & 3]; };
+  auto tile = [&](const f32x4 (&A)[NV], int64_t t) {
     f32x16 acc = {};
 #pragma unroll
-    for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], bq[s], acc, 0, 0, 0);
-
+    for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(A, s), bq[s], acc, 0, 0, 0);
     float m = fminf(fminf(fminf(acc[0], acc[1]), fminf(acc[2], acc[3])),
                     fminf(fminf(acc[4], acc[5]), fminf(acc[6], acc[7])));
     m = fminf(m, fminf(fminf(fminf(acc[8], acc[9]), fminf(acc[10], acc[11])),
@@ -206,6 +226,21 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ a
       }
       if (__ballot(cnt > kBufCap - 16)) flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l);
     }
+  };
+  if (t0 < t1) {
+    load(A0, t0);
+    int64_t t = t0;
+#pragma nounroll
+    for (; t + 1 < t1; t += 2) {
+      load(A1, t + 1);
+      wait_older(A0);
+      tile(A0, t);
+      load(A0, min(t + 2, t1 - 1));
+      wait_older(A1);
+      tile(A1, t + 1);
+    }
+    wait_all(A0);
+    if (t < t1) tile(A0, t);
   }
   flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l);
 
