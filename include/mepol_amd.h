@@ -101,19 +101,29 @@ int mepol_entropy_reverse_scan(const double* gamma, const double* w, const doubl
                                int64_t num_traj, int64_t T_stride, const double* grad_H,
                                double* grad_logp, void* stream);
 
-/* ---- Gaussian policy head (GaussianPolicy.get_log_p, src/policy.py:43-51) ----------------
- * Fused mean layer + log-probability with the last hidden ReLU folded in: z [n, hidden] is the
- * last hidden layer's PRE-activation; Wm [a_dim, hidden], bm/log_std [a_dim]; act [n, a_dim].
- * Forward writes mu [n, a_dim] and logp [n].  Backward (grad_logp [n]) writes dz [n, hidden]
- * (nullable), dWm, dbm, dlog_std.  Limits: hidden <= 512, a_dim <= 8. */
-int mepol_head_forward(const double* z, int64_t n, int hidden, const double* Wm, const double* bm,
-                       const double* log_std, const double* act, int a_dim, double* mu_out,
-                       double* logp_out, void* stream);
+/* ---- policy MLP (GaussianPolicy, src/policy.py:16-51) for the large-batch passes -----------
+ * Gaussian head: mean layer + log-probability with the last hidden layer's bias and ReLU folded
+ * in.  z [n, hidden] is the last hidden layer's PRE-activation WITHOUT its bias bz (nullable);
+ * Wm [a_dim, hidden], bm/log_std [a_dim]; act [n, a_dim].  Forward writes mu [n, a_dim] and
+ * logp [n].  Backward (grad_logp [n]) writes dz [n, hidden] (nullable), dWm, dbm, dlog_std and
+ * dbz [hidden] (nullable).  Limits: hidden <= 512, a_dim <= 8. */
+int mepol_head_forward(const double* z, int64_t n, int hidden, const double* bz, const double* Wm,
+                       const double* bm, const double* log_std, const double* act, int a_dim,
+                       double* mu_out, double* logp_out, void* stream);
 int mepol_head_workspace_size(int64_t n, int hidden, int a_dim, size_t* bytes);
 int mepol_head_backward(const double* grad_logp, const double* z, int64_t n, int hidden,
-                        const double* Wm, const double* log_std, const double* act,
-                        const double* mu, int a_dim, double* dz, double* dWm, double* dbm,
-                        double* dlog_std, void* workspace, size_t workspace_bytes, void* stream);
+                        const double* bz, const double* Wm, const double* log_std,
+                        const double* act, const double* mu, int a_dim, double* dz, double* dWm,
+                        double* dbm, double* dlog_std, double* dbz, void* workspace,
+                        size_t workspace_bytes, void* stream);
+/* Input layer h = relu(x W^T + b): x [n, in] (in <= 64), W [out, in], b [out], h [n, out];
+ * backward from dh = dL/dh and h: dW [out, in], db [out] (nullable). */
+int mepol_layer_forward(const double* x, int64_t n, int in_features, const double* W,
+                        const double* b, int out_features, double* h_out, void* stream);
+int mepol_layer_workspace_size(int64_t n, int in_features, int out_features, size_t* bytes);
+int mepol_layer_backward(const double* dh, const double* h, const double* x, int64_t n,
+                         int in_features, int out_features, double* dW, double* db,
+                         void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- environments -------------------------------------------------------------------------
  * Replace MountainCarContinuous.step (src/envs/mountain_car_wall.py:13-45) and

@@ -39,11 +39,15 @@ SIGNATURES = {
     "mepol_entropy_gamma": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp],
     "mepol_entropy_reverse_scan": [_c_vp, _c_vp, _c_vp, _c_i64, _c_vp, _c_vp, _c_i64, _c_i64,
                                    _c_vp, _c_vp, _c_vp],
-    "mepol_head_forward": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
-                           _c_vp],
+    "mepol_head_forward": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp,
+                           _c_vp, _c_vp],
     "mepol_head_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
-    "mepol_head_backward": [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp,
-                            _c_vp, _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
+    "mepol_head_backward": [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int,
+                            _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
+    "mepol_layer_forward": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp],
+    "mepol_layer_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
+    "mepol_layer_backward": [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_sz,
+                             _c_vp],
     "mepol_step_mountaincar": [_c_vp, _c_vp, _c_i64, _c_i64, _c_vp],
     "mepol_step_gridworld": [_c_vp, _c_vp, _c_i64, _c_vp],
     "mepol_rollout_step": [_c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_i64,

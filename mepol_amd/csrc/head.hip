@@ -62,7 +62,8 @@ __device__ __forceinline__ double reduce_scatter(double (&v)[AP], int l, int& a_
 // current row's math), so the kernel streams z at HBM rate with no LDS traffic.
 template <int AP, int NC>
 __global__ __launch_bounds__(256) void head_fwd_kernel(
-    const double* __restrict__ z, int64_t N, int H, const double* __restrict__ Wm,
+    const double* __restrict__ z, int64_t N, int H, const double* __restrict__ bz,
+    const double* __restrict__ Wm,
     const double* __restrict__ bm, const double* __restrict__ log_std,
     const double* __restrict__ act, int A, double* __restrict__ mu_out,
     double* __restrict__ logp_out) {
@@ -76,6 +77,9 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
     sW[e] = (c < H && a < A) ? Wm[a * H + c] : 0.0;
   }
   __syncthreads();
+  double bzr[NC];  // last hidden layer's bias, folded in here (its GEMM runs without bias)
+#pragma unroll
+  for (int j = 0; j < NC; ++j) bzr[j] = (bz && l + 64 * j < H) ? bz[l + 64 * j] : 0.0;
   double zn[NC];
   auto load_row = [&](int64_t i) {
 #pragma unroll
@@ -111,7 +115,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
     asm volatile("" : "+v"(lo));  // keep the Wm LDS reads in the loop (no hoist into VGPRs)
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
-      const double x = fmax(zc[j], 0.0);
+      const double x = fmax(zc[j] + bzr[j], 0.0);
 #pragma unroll
       for (int a = 0; a < AP; ++a) acc[a] += x * sW[(j * AP + a) * 64 + lo];
     }
@@ -143,11 +147,11 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(
 template <int AP, int NC>
 __global__ __launch_bounds__(256) void head_bwd_kernel(
     const double* __restrict__ gl, const double* __restrict__ z, int64_t N, int H,
-    const double* __restrict__ Wm, const double* __restrict__ log_std,
+    const double* __restrict__ bz, const double* __restrict__ Wm, const double* __restrict__ log_std,
     const double* __restrict__ act, const double* __restrict__ mu, int A,
     double* __restrict__ dz, double* __restrict__ part) {
   __shared__ double sW[NC * 64 * AP];   // [j][a][lane]
-  __shared__ double sRed[AP * 64 * NC];  // block accumulator, waves add in order 0..3
+  __shared__ double sRed[AP * 64 * NC + 64 * NC];  // block accumulators, waves add in order 0..3
   __shared__ double sb[4][AP], sls[4][AP];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -178,6 +182,12 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
 #pragma unroll
     for (int a = 0; a < AP; ++a) accW[j][a] = 0.0;
   double accb = 0.0, accls = 0.0;  // lane a (< A) accumulates component a
+  double bzr[NC], accz[NC];         // folded bias of z and its gradient (column sums of dz)
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    bzr[j] = (bz && l + 64 * j < H) ? bz[l + 64 * j] : 0.0;
+    accz[j] = 0.0;
+  }
   double zn[NC];
   auto load_row = [&](int64_t i) {
 #pragma unroll
@@ -217,14 +227,17 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
       const int c = l + 64 * j;
-      const double x = fmax(zc[j], 0.0);
+      const double zb = zc[j] + bzr[j];
+      const double x = fmax(zb, 0.0);
       double dh = 0.0;
 #pragma unroll
       for (int a = 0; a < AP; ++a) {
         dh += dm[a] * sW[(j * AP + a) * 64 + lo];
         accW[j][a] += dm[a] * x;
       }
-      if (dzr && c < H) dzr[c] = (zc[j] > 0.0) ? dh : 0.0;
+      const double dzv = (zb > 0.0) ? dh : 0.0;
+      accz[j] += dzv;
+      if (dzr && c < H) dzr[c] = dzv;
     }
   }
   // block reduction in a fixed order (waves 0..3), then one record per block
@@ -257,6 +270,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     rec[A * H + a] = ((sb[0][a] + sb[1][a]) + sb[2][a]) + sb[3][a];
     rec[A * H + A + a] = ((sls[0][a] + sls[1][a]) + sls[2][a]) + sls[3][a];
   }
+  for (int c = threadIdx.x; c < H; c += blockDim.x) rec[A * H + 2 * A + c] = sRed[AP * 64 * NC + c];
 }
 
 // out = sum_b part[b][:] in a fixed order: 64 elements per block, wave w sums a quarter of the
@@ -265,7 +279,8 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __re
                                                               int nblocks, int64_t m, int AH,
                                                               int A, double* __restrict__ dWm,
                                                               double* __restrict__ dbm,
-                                                              double* __restrict__ dls) {
+                                                              double* __restrict__ dls,
+                                                              double* __restrict__ dbz) {
   __shared__ double sh[4][64];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t e = (int64_t)blockIdx.x * 64 + l;
@@ -282,8 +297,10 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __re
       dWm[e] = t;
     else if (e < AH + A)
       dbm[e - AH] = t;
-    else
+    else if (e < AH + 2 * A)
       dls[e - AH - A] = t;
+    else if (dbz)
+      dbz[e - AH - 2 * A] = t;
   }
 }
 
@@ -302,9 +319,10 @@ static int grid_bwd(int64_t N) {
 using namespace mepol;
 using namespace mepol::head;
 
-extern "C" int mepol_head_forward(const double* z, int64_t n, int hidden, const double* Wm,
-                                  const double* bm, const double* log_std, const double* act,
-                                  int a_dim, double* mu_out, double* logp_out, void* stream) {
+extern "C" int mepol_head_forward(const double* z, int64_t n, int hidden, const double* bz,
+                                  const double* Wm, const double* bm, const double* log_std,
+                                  const double* act, int a_dim, double* mu_out, double* logp_out,
+                                  void* stream) {
   if (n < 0 || hidden <= 0 || hidden > 64 * kMaxCols || a_dim <= 0 || a_dim > kMaxA || !z ||
       !Wm || !bm || !log_std || !act || !mu_out || !logp_out) {
     set_error("mepol_head_forward: bad arguments (hidden <= 512, action_dim <= 8)");
@@ -317,8 +335,8 @@ extern "C" int mepol_head_forward(const double* z, int64_t n, int hidden, const 
   hipStream_t st = (hipStream_t)stream;
 #define MEPOL_HEAD_FWD(AP_, NC_)                                                                \
   if (ap == AP_ && nc == NC_)                                                                   \
-    hipLaunchKernelGGL((head_fwd_kernel<AP_, NC_>), g, dim3(256), 0, st, z, n, hidden, Wm, bm,  \
-                       log_std, act, a_dim, mu_out, logp_out);
+    hipLaunchKernelGGL((head_fwd_kernel<AP_, NC_>), g, dim3(256), 0, st, z, n, hidden, bz, Wm,  \
+                       bm, log_std, act, a_dim, mu_out, logp_out);
 #define MEPOL_HEAD_FWD_A(AP_) \
   MEPOL_HEAD_FWD(AP_, 1) MEPOL_HEAD_FWD(AP_, 2) MEPOL_HEAD_FWD(AP_, 3) MEPOL_HEAD_FWD(AP_, 4) \
   MEPOL_HEAD_FWD(AP_, 5) MEPOL_HEAD_FWD(AP_, 6) MEPOL_HEAD_FWD(AP_, 7) MEPOL_HEAD_FWD(AP_, 8)
@@ -332,17 +350,17 @@ extern "C" int mepol_head_forward(const double* z, int64_t n, int hidden, const 
 extern "C" int mepol_head_workspace_size(int64_t n, int hidden, int a_dim, size_t* bytes) {
   if (!bytes || hidden <= 0 || a_dim <= 0) return kErrBadArg;
   const int nb = grid_bwd(std::max<int64_t>(n, 1));
-  *bytes = (size_t)nb * a_dim * (hidden + 2) * sizeof(double);
+  *bytes = (size_t)nb * ((size_t)a_dim * (hidden + 2) + hidden) * sizeof(double);
   return 0;
 }
 
 // dz [n, hidden] (nullable: skip the input gradient), dWm [a_dim, hidden], dbm [a_dim],
 // dlog_std [a_dim] are written (not accumulated).
 extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int64_t n, int hidden,
-                                   const double* Wm, const double* log_std, const double* act,
-                                   const double* mu, int a_dim, double* dz, double* dWm,
-                                   double* dbm, double* dlog_std, void* workspace,
-                                   size_t workspace_bytes, void* stream) {
+                                   const double* bz, const double* Wm, const double* log_std,
+                                   const double* act, const double* mu, int a_dim, double* dz,
+                                   double* dWm, double* dbm, double* dlog_std, double* dbz,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
   if (n <= 0 || hidden <= 0 || hidden > 64 * kMaxCols || a_dim <= 0 || a_dim > kMaxA ||
       !grad_logp || !z || !Wm || !log_std || !act || !mu || !dWm || !dbm || !dlog_std ||
       !workspace) {
@@ -350,7 +368,7 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
     return kErrBadArg;
   }
   const int nb = grid_bwd(n);
-  const size_t need = (size_t)nb * a_dim * (hidden + 2) * sizeof(double);
+  const size_t need = (size_t)nb * ((size_t)a_dim * (hidden + 2) + hidden) * sizeof(double);
   if (workspace_bytes < need) {
     set_error("mepol_head_backward: workspace %zu < %zu", workspace_bytes, need);
     return kErrWorkspace;
@@ -363,7 +381,7 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
 #define MEPOL_HEAD_BWD(AP_, NC_)                                                                  \
   if (ap == AP_ && nc == NC_)                                                                     \
     hipLaunchKernelGGL((head_bwd_kernel<AP_, NC_>), g, dim3(256), 0, st, grad_logp, z, n, hidden, \
-                       Wm, log_std, act, mu, a_dim, dz, pdW);
+                       bz, Wm, log_std, act, mu, a_dim, dz, pdW);
 #define MEPOL_HEAD_BWD_A(AP_) \
   MEPOL_HEAD_BWD(AP_, 1) MEPOL_HEAD_BWD(AP_, 2) MEPOL_HEAD_BWD(AP_, 3) MEPOL_HEAD_BWD(AP_, 4) \
   MEPOL_HEAD_BWD(AP_, 5) MEPOL_HEAD_BWD(AP_, 6) MEPOL_HEAD_BWD(AP_, 7) MEPOL_HEAD_BWD(AP_, 8)
@@ -371,9 +389,9 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
 #undef MEPOL_HEAD_BWD_A
 #undef MEPOL_HEAD_BWD
   MEPOL_CHECK_LAUNCH();
-  const int64_t m = (int64_t)a_dim * hidden + 2 * a_dim;
+  const int64_t m = (int64_t)a_dim * hidden + 2 * a_dim + hidden;
   hipLaunchKernelGGL(reduce_partials_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st, pdW,
-                     nb, m, a_dim * hidden, a_dim, dWm, dbm, dlog_std);
+                     nb, m, a_dim * hidden, a_dim, dWm, dbm, dlog_std, dbz);
   MEPOL_CHECK_LAUNCH();
   return 0;
 }

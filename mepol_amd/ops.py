@@ -185,18 +185,19 @@ def entropy_reverse_scan(gamma, w, partials, nparts, offsets, nt, T_stride, grad
     return grad
 
 
-def head_forward(z, Wm, bm, log_std, act):
-    """Fused Gaussian head: returns (mu [n, a], logp [n]) from the last PRE-activation z."""
+def head_forward(z, Wm, bm, log_std, act, bz=None):
+    """Fused Gaussian head: (mu [n, a], logp [n]) from the last pre-activation z (+ bias bz)."""
     n, h = z.shape
     a = Wm.shape[0]
     mu = torch.empty((n, a), dtype=torch.float64, device=z.device)
     logp = torch.empty(n, dtype=torch.float64, device=z.device)
-    call("mepol_head_forward", ptr(z), n, h, ptr(Wm), ptr(bm), ptr(log_std), ptr(act), a, ptr(mu),
-         ptr(logp), _stream())
+    call("mepol_head_forward", ptr(z), n, h, ptr(bz), ptr(Wm), ptr(bm), ptr(log_std), ptr(act), a,
+         ptr(mu), ptr(logp), _stream())
     return mu, logp
 
 
-def head_backward(grad_logp, z, Wm, log_std, act, mu, need_dz=True):
+def head_backward(grad_logp, z, Wm, log_std, act, mu, bz=None, need_dz=True):
+    """Returns (dz or None, dWm, dbm, dlog_std, dbz or None)."""
     import ctypes
 
     n, h = z.shape
@@ -209,9 +210,35 @@ def head_backward(grad_logp, z, Wm, log_std, act, mu, need_dz=True):
     dWm = torch.empty_like(Wm)
     dbm = torch.empty(a, dtype=torch.float64, device=dev)
     dls = torch.empty(a, dtype=torch.float64, device=dev)
-    call("mepol_head_backward", ptr(grad_logp), ptr(z), n, h, ptr(Wm), ptr(log_std), ptr(act),
-         ptr(mu), a, ptr(dz), ptr(dWm), ptr(dbm), ptr(dls), ptr(ws), ws.numel(), _stream())
-    return dz, dWm, dbm, dls
+    dbz = torch.empty(h, dtype=torch.float64, device=dev) if bz is not None else None
+    call("mepol_head_backward", ptr(grad_logp), ptr(z), n, h, ptr(bz), ptr(Wm), ptr(log_std),
+         ptr(act), ptr(mu), a, ptr(dz), ptr(dWm), ptr(dbm), ptr(dls), ptr(dbz), ptr(ws), ws.numel(),
+         _stream())
+    return dz, dWm, dbm, dls, dbz
+
+
+def layer_forward(x, W, b):
+    """h = relu(x W^T + b) for the policy's input layer (in_features <= 64)."""
+    n, f = x.shape
+    h = torch.empty((n, W.shape[0]), dtype=torch.float64, device=x.device)
+    call("mepol_layer_forward", ptr(x), n, f, ptr(W), ptr(b), W.shape[0], ptr(h), _stream())
+    return h
+
+
+def layer_backward(dh, h, x):
+    """(dW, db) of h = relu(x W^T + b) from dL/dh and the forward output h."""
+    import ctypes
+
+    n, f = x.shape
+    out = h.shape[1]
+    nbytes = ctypes.c_size_t()
+    call("mepol_layer_workspace_size", n, f, out, ctypes.byref(nbytes))
+    ws = _workspace(x.device, nbytes.value, tag="layer")
+    dW = torch.empty((out, f), dtype=torch.float64, device=x.device)
+    db = torch.empty(out, dtype=torch.float64, device=x.device)
+    call("mepol_layer_backward", ptr(dh), ptr(h), ptr(x), n, f, out, ptr(dW), ptr(db), ptr(ws),
+         ws.numel(), _stream())
+    return dW, db
 
 
 def step_mountaincar(state, action):

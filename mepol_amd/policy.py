@@ -72,9 +72,41 @@ class _HeadLogp(torch.autograd.Function):
         from . import ops
 
         z, w_mean, log_std, actions, mu = ctx.saved_tensors
-        dz, dw, db, dls = ops.head_backward(g.contiguous(), z, w_mean, log_std, actions, mu,
-                                            need_dz=ctx.needs_input_grad[0])
+        dz, dw, db, dls, _ = ops.head_backward(g.contiguous(), z, w_mean, log_std, actions, mu,
+                                               need_dz=ctx.needs_input_grad[0])
         return dz, dw, db, dls, None
+
+
+class _TwoLayerLogp(torch.autograd.Function):
+    """log p(a | s) of the reference's 2-hidden-layer ReLU policy for a large batch:
+
+    layer 1  h1 = relu(x W1^T + b1)            HIP (csrc/mlp.hip), bias + ReLU fused
+    layer 2  z2 = h1 W2^T                       rocBLAS GEMM without bias
+    head     logp(relu(z2 + b2) Wm^T + bm)      HIP (csrc/head.hip), b2 + ReLU folded in
+    backward: head (dz2, dWm, dbm, dlog_std, db2 in one pass) -> dW2 split-K bmm, dh1 GEMM ->
+    layer-1 weights (ReLU mask, dW1, db1 in one pass).  Same math as nn.Linear/ReLU."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, b2, Wm, bm, log_std, actions):
+        from . import ops
+
+        h1 = ops.layer_forward(x, W1, b1)
+        z2 = torch.mm(h1, W2.t())
+        mu, logp = ops.head_forward(z2, Wm, bm, log_std, actions, bz=b2)
+        ctx.save_for_backward(x, h1, z2, W2, b2, Wm, log_std, actions, mu)
+        return logp
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import ops
+
+        x, h1, z2, W2, b2, Wm, log_std, actions, mu = ctx.saved_tensors
+        dz2, dWm, dbm, dls, db2 = ops.head_backward(g.contiguous(), z2, Wm, log_std, actions, mu,
+                                                    bz=b2, need_dz=True)
+        dW2 = _weight_grad(dz2, h1)
+        dh1 = torch.mm(dz2, W2)
+        dW1, db1 = ops.layer_backward(dh1, h1, x)
+        return None, dW1, db1, dW2, db2, dWm, dbm, dls, None
 
 
 def _apply_linear(layer, x):
@@ -126,6 +158,11 @@ class GaussianPolicy(nn.Module):
         """sum_a -0.5 (log 2pi + 2 log_std + (a - mu)^2 / (exp(log_std) + 1e-7)^2)."""
         if self._fused_head_ok(states, actions):
             layers = [m for m in self.net if isinstance(m, nn.Linear)]
+            if len(layers) == 2 and self.num_features <= 64:
+                l1, l2 = layers
+                return _TwoLayerLogp.apply(states.contiguous(), l1.weight.contiguous(), l1.bias,
+                                           l2.weight, l2.bias, self.mean.weight.contiguous(),
+                                           self.mean.bias, self.log_std, actions.contiguous())
             h = states
             for layer in layers[:-1]:
                 h = torch.relu(_apply_linear(layer, h))

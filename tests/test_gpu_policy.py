@@ -31,3 +31,28 @@ def test_fused_head_matches_unfused(cuda, nf, hidden, a):
         assert torch.allclose(g_fused[k], v.grad, rtol=1e-10, atol=1e-12 * v.grad.abs().max()), k
     with torch.no_grad():
         assert torch.allclose(pol.get_log_p(s, act), ref, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("nf,hidden,a", [(29, [400, 300], 8), (2, [300, 300], 2), (7, [130, 70], 3)])
+def test_two_layer_fused_path_matches_nn_modules(cuda, nf, hidden, a):
+    """The _TwoLayerLogp path (HIP layer 1 + rocBLAS layer 2 + HIP head) == nn.Linear/ReLU."""
+    from mepol_amd import policy as P
+
+    torch.manual_seed(1)
+    pol = P.GaussianPolicy(hidden, nf, a, -0.3).cuda()
+    n = 30000
+    s = torch.randn(n, nf, dtype=torch.float64, device="cuda")
+    act = 0.5 * torch.randn(n, a, dtype=torch.float64, device="cuda")
+    coef = torch.randn(n, dtype=torch.float64, device="cuda")
+    lp = pol.get_log_p(s, act)
+    assert lp.grad_fn is not None and "TwoLayer" in type(lp.grad_fn).__name__
+    (coef * lp).sum().backward()
+    got = {k: v.grad.clone() for k, v in pol.named_parameters()}
+    pol.zero_grad()
+    mu = pol.mean(pol.net(s))
+    std = torch.exp(pol.log_std) + 1e-7
+    ref = torch.sum(-0.5 * (P.LOG_2PI + 2 * pol.log_std + (act - mu) ** 2 / std ** 2), dim=1)
+    (coef * ref).sum().backward()
+    assert torch.allclose(lp, ref, rtol=1e-12, atol=1e-12)
+    for k, v in pol.named_parameters():
+        assert torch.allclose(got[k], v.grad, rtol=1e-10, atol=1e-12 * v.grad.abs().max()), k
