@@ -257,7 +257,19 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     }
     __syncthreads();
   }
-  const int64_t m = (int64_t)A * H + 2 * A;
+  // column sums of dz, same fixed wave order, in the tail of sRed
+  for (int ww = 0; ww < 4; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (int j = 0; j < NC; ++j) {
+        const int idx = AP * 64 * NC + j * 64 + l;
+        sRed[idx] = (ww == 0 ? 0.0 : sRed[idx]) + accz[j];
+      }
+    }
+    __syncthreads();
+  }
+  // partial record: [dW (A*H) | db (A) | dls (A) | dbz (H)]
+  const int64_t m = (int64_t)A * H + 2 * A + H;
   double* rec = part + (int64_t)blockIdx.x * m;
   for (int e = threadIdx.x; e < A * H; e += blockDim.x) {
     const int a = e / H, c = e % H;
