@@ -14,11 +14,28 @@
 namespace mepol {
 namespace mlp {
 
+constexpr int kChunk = 64;  // rows staged per block iteration
+
+// Stage kChunk rows of x (contiguous kChunk*F doubles) into LDS with coalesced loads; features
+// [F, FP) stay zero so the unrolled FMA chain needs no per-feature guard.
+template <int FP>
+__device__ __forceinline__ int stage_rows(const double* __restrict__ x, int64_t N, int F,
+                                          int64_t r0, double (*sx)[FP]) {
+  const int nrow = (int)min<int64_t>(kChunk, N - r0);
+  const double* src = x + r0 * F;
+  for (int e = threadIdx.x; e < nrow * F; e += blockDim.x) {
+    const int rr = e / F;
+    sx[rr][e - rr * F] = src[e];
+  }
+  return nrow;
+}
+
 template <int FP>
 __global__ __launch_bounds__(256) void layer_fwd_kernel(const double* __restrict__ x, int64_t N,
                                                         int F, const double* __restrict__ W,
                                                         const double* __restrict__ b, int H,
                                                         double* __restrict__ h) {
+  __shared__ double sx[kChunk][FP];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + l;
   const bool col = c < H;
@@ -26,15 +43,17 @@ __global__ __launch_bounds__(256) void layer_fwd_kernel(const double* __restrict
 #pragma unroll
   for (int f = 0; f < FP; ++f) wr[f] = (col && f < F) ? W[(int64_t)c * F + f] : 0.0;
   const double bc = col ? b[c] : 0.0;
-  const int64_t stride = (int64_t)gridDim.x * 4;
-  const int64_t r0 = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + w));
-  for (int64_t r = r0; r < N; r += stride) {
-    const double* xr = x + r * F;  // wave-uniform address -> scalar loads
-    double acc = bc;
+  for (int e = threadIdx.x; e < kChunk * FP; e += blockDim.x) sx[e / FP][e % FP] = 0.0;
+  for (int64_t r0 = (int64_t)blockIdx.x * kChunk; r0 < N; r0 += (int64_t)gridDim.x * kChunk) {
+    __syncthreads();
+    const int nrow = stage_rows<FP>(x, N, F, r0, sx);
+    __syncthreads();
+    for (int rr = w; rr < nrow; rr += 4) {
+      double acc = bc;
 #pragma unroll
-    for (int f = 0; f < FP; ++f)
-      if (f < F) acc = fma(xr[f], wr[f], acc);
-    if (col) h[r * H + c] = fmax(acc, 0.0);
+      for (int f = 0; f < FP; ++f) acc = fma(sx[rr][f], wr[f], acc);
+      if (col) h[(r0 + rr) * H + c] = fmax(acc, 0.0);
+    }
   }
 }
 
@@ -44,36 +63,44 @@ __global__ __launch_bounds__(256) void layer_bwd_kernel(const double* __restrict
                                                         const double* __restrict__ h,
                                                         const double* __restrict__ x, int64_t N,
                                                         int F, int H, double* __restrict__ part) {
-  __shared__ double sacc[4][64][FP + 1];
+  __shared__ double sx[kChunk][FP];
+  __shared__ double sacc[64][FP + 1];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + l;
   const bool col = c < H;
   double acc[FP], accb = 0.0;
 #pragma unroll
   for (int f = 0; f < FP; ++f) acc[f] = 0.0;
-  const int64_t stride = (int64_t)gridDim.x * 4;
-  const int64_t r0 = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + w));
-  for (int64_t r = r0; r < N; r += stride) {
-    double dz = 0.0;
-    if (col) {
-      const double hv = h[r * H + c];
-      dz = (hv > 0.0) ? dh[r * H + c] : 0.0;
+  for (int e = threadIdx.x; e < kChunk * FP; e += blockDim.x) sx[e / FP][e % FP] = 0.0;
+  for (int64_t r0 = (int64_t)blockIdx.x * kChunk; r0 < N; r0 += (int64_t)gridDim.x * kChunk) {
+    __syncthreads();
+    const int nrow = stage_rows<FP>(x, N, F, r0, sx);
+    __syncthreads();
+    for (int rr = w; rr < nrow; rr += 4) {
+      double dz = 0.0;
+      if (col) {
+        const int64_t o = (r0 + rr) * H + c;
+        const double hv = h[o];
+        dz = (hv > 0.0) ? dh[o] : 0.0;
+      }
+#pragma unroll
+      for (int f = 0; f < FP; ++f) acc[f] = fma(dz, sx[rr][f], acc[f]);
+      accb += dz;
     }
-    const double* xr = x + r * F;
-#pragma unroll
-    for (int f = 0; f < FP; ++f)
-      if (f < F) acc[f] = fma(dz, xr[f], acc[f]);
-    accb += dz;
   }
+  // Fixed-order cross-wave sum: wave 0 writes, waves 1..3 add in turn.
+  for (int ww = 0; ww < 4; ++ww) {
+    if (w == ww) {
 #pragma unroll
-  for (int f = 0; f < FP; ++f) sacc[w][l][f] = acc[f];
-  sacc[w][l][FP] = accb;
-  __syncthreads();
+      for (int f = 0; f < FP; ++f) sacc[l][f] = (ww == 0) ? acc[f] : sacc[l][f] + acc[f];
+      sacc[l][FP] = (ww == 0) ? accb : sacc[l][FP] + accb;
+    }
+    __syncthreads();
+  }
   if (w == 0 && col) {
     double* rec = part + ((int64_t)blockIdx.x * H + c) * (F + 1);
-    for (int f = 0; f < F; ++f)
-      rec[f] = ((sacc[0][l][f] + sacc[1][l][f]) + sacc[2][l][f]) + sacc[3][l][f];
-    rec[F] = ((sacc[0][l][FP] + sacc[1][l][FP]) + sacc[2][l][FP]) + sacc[3][l][FP];
+    for (int f = 0; f < F; ++f) rec[f] = sacc[l][f];
+    rec[F] = sacc[l][FP];
   }
 }
 
@@ -92,7 +119,7 @@ __global__ void layer_reduce_kernel(const double* __restrict__ part, int nb, int
     db[c] = s;
 }
 
-constexpr int kRowBlocks = 128;  // blocks along the rows (x 4 waves): 512 row streams per column tile
+constexpr int kRowBlocks = 256;  // row-chunk blocks per column tile (grid-stride over chunks)
 
 }  // namespace mlp
 }  // namespace mepol
@@ -130,7 +157,7 @@ extern "C" int mepol_layer_forward(const double* x, int64_t n, int in_features, 
     return kErrBadArg;
   }
   if (n == 0) return 0;
-  const int gx = (int)std::min<int64_t>(kRowBlocks, (n + 3) / 4);
+  const int gx = (int)std::min<int64_t>(kRowBlocks, (n + kChunk - 1) / kChunk);
   dim3 g(gx, (out_features + 63) / 64);
   hipStream_t st = (hipStream_t)stream;
   MEPOL_FP_SWITCH(in_features, hipLaunchKernelGGL((layer_fwd_kernel<FP>), g, dim3(256), 0, st, x,
@@ -142,7 +169,7 @@ extern "C" int mepol_layer_forward(const double* x, int64_t n, int in_features, 
 extern "C" int mepol_layer_workspace_size(int64_t n, int in_features, int out_features,
                                           size_t* bytes) {
   if (!bytes || in_features <= 0 || out_features <= 0) return kErrBadArg;
-  const int gx = (int)std::min<int64_t>(kRowBlocks, std::max<int64_t>((n + 3) / 4, 1));
+  const int gx = (int)std::min<int64_t>(kRowBlocks, std::max<int64_t>((n + kChunk - 1) / kChunk, 1));
   *bytes = (size_t)gx * out_features * (in_features + 1) * sizeof(double);
   return 0;
 }
@@ -156,7 +183,7 @@ extern "C" int mepol_layer_backward(const double* dh, const double* h, const dou
     set_error("mepol_layer_backward: bad arguments");
     return kErrBadArg;
   }
-  const int gx = (int)std::min<int64_t>(kRowBlocks, (n + 3) / 4);
+  const int gx = (int)std::min<int64_t>(kRowBlocks, (n + kChunk - 1) / kChunk);
   const size_t need = (size_t)gx * out_features * (in_features + 1) * sizeof(double);
   if (workspace_bytes < need) {
     set_error("mepol_layer_backward: workspace %zu < %zu", workspace_bytes, need);
