@@ -218,14 +218,10 @@ def compute_entropy(behavioral_policy, target_policy, states, actions, num_traj,
     return H
 
 
-def compute_kl(behavioral_policy, target_policy, states, actions, num_traj, real_traj_lengths,
-               distances, indices, k, eps):
-    """k-NN KL(behavioral || target) estimate and its numeric-error flag (mepol.py:157-174).
-
-    When gradients are enabled, the target policy's MLP forward is kept (with its graph) so a
-    following policy_update at the same parameters reuses it instead of recomputing it; the
-    returned values are those of the reference's no_grad computation.
-    """
+def compute_kl_deferred(behavioral_policy, target_policy, states, actions, num_traj,
+                        real_traj_lengths, distances, indices, k, eps):
+    """compute_kl with the numeric-error flag left on the device (a 0-d bool tensor), so the
+    off-policy loop reads every control scalar of an iteration with one synchronisation."""
     batch = P.lookup(states, actions, real_traj_lengths, distances, indices)
     logp_b = batch.behavioral_logp(behavioral_policy)
     if target_policy is behavioral_policy:
@@ -240,9 +236,33 @@ def compute_kl(behavioral_policy, target_policy, states, actions, num_traj, real
         _, _, w, _ = ops.iw_forward(logp_t.detach(), logp_b, batch.offsets, batch.N)
         out4, _, _ = ops.entropy_forward(w, batch.idx32T, batch.D, k, 1.0, 1.0, 0.0, eps)
     kl = out4[1].clone()
-    numeric_error = bool(torch.isinf(kl) or torch.isnan(kl))
-    kl = torch.clamp_min(kl, 0.0)
-    return kl, numeric_error
+    return torch.clamp_min(kl, 0.0), ~torch.isfinite(kl)
+
+
+def compute_kl(behavioral_policy, target_policy, states, actions, num_traj, real_traj_lengths,
+               distances, indices, k, eps):
+    """k-NN KL(behavioral || target) estimate and its numeric-error flag (mepol.py:157-174).
+
+    When gradients are enabled, the target policy's MLP forward is kept (with its graph) so a
+    following policy_update at the same parameters reuses it instead of recomputing it; the
+    returned values are those of the reference's no_grad computation.
+    """
+    kl, flag = compute_kl_deferred(behavioral_policy, target_policy, states, actions, num_traj,
+                                   real_traj_lengths, distances, indices, k, eps)
+    return kl, bool(flag)
+
+
+def policy_update_deferred(optimizer, behavioral_policy, target_policy, states, actions, num_traj,
+                           traj_len, distances, indices, k, G, B, ns, eps):
+    """policy_update with the numeric-error flag (taken on the loss before backward, as at
+    mepol.py:274-276) left on the device as a 0-d bool tensor."""
+    optimizer.zero_grad()
+    loss = -compute_entropy(behavioral_policy, target_policy, states, actions, num_traj, traj_len,
+                            distances, indices, k, G, B, ns, eps)
+    flag = ~torch.isfinite(loss.detach())
+    loss.backward()
+    optimizer.step()
+    return loss, flag
 
 
 def policy_update(optimizer, behavioral_policy, target_policy, states, actions, num_traj, traj_len,
@@ -252,13 +272,10 @@ def policy_update(optimizer, behavioral_policy, target_policy, states, actions, 
     The 5th positional argument is the real trajectory lengths, as at the reference call site
     (mepol.py:429-431).
     """
-    optimizer.zero_grad()
-    loss = -compute_entropy(behavioral_policy, target_policy, states, actions, num_traj, traj_len,
-                            distances, indices, k, G, B, ns, eps)
-    numeric_error = bool(torch.isinf(loss) or torch.isnan(loss))
-    loss.backward()
-    optimizer.step()
-    return loss, numeric_error
+    loss, flag = policy_update_deferred(optimizer, behavioral_policy, target_policy, states,
+                                        actions, num_traj, traj_len, distances, indices, k, G, B,
+                                        ns, eps)
+    return loss, bool(flag)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -478,25 +495,44 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
     else:
         backtrack_iter = None
 
+    deferred = hasattr(fns, "policy_update_deferred") and hasattr(fns, "compute_kl_deferred")
+    if fns is sys.modules[__name__]:
+        # A caller that replaced policy_update / compute_kl (reference-style patching) gets
+        # its functions called, not the deferred built-ins.
+        deferred = (fns.policy_update, fns.compute_kl) == _BUILTIN_STEP_FNS
     while not kl_threshold_reached:
-        loss, numeric_error = fns.policy_update(optimizer, behavioral_policy, target_policy, states,
-                                                actions, num_traj, real_traj_lengths, distances,
-                                                indices, k, G, B, ns, eps)
-        entropy = -_np(loss)
-        kl, kl_numeric_error = fns.compute_kl(behavioral_policy, target_policy, states, actions,
-                                              num_traj, real_traj_lengths, distances, indices, k,
-                                              eps)
-        kl = _np(kl)
+        if deferred:
+            # Queue the update and the KL pass, then read all four control scalars at once.
+            loss, loss_flag = fns.policy_update_deferred(
+                optimizer, behavioral_policy, target_policy, states, actions, num_traj,
+                real_traj_lengths, distances, indices, k, G, B, ns, eps)
+            kl, kl_flag = fns.compute_kl_deferred(behavioral_policy, target_policy, states,
+                                                  actions, num_traj, real_traj_lengths,
+                                                  distances, indices, k, eps)
+            vals = torch.stack([loss.detach().reshape(()), kl.reshape(()),
+                                loss_flag.reshape(()).to(loss.dtype),
+                                kl_flag.reshape(()).to(loss.dtype)]).cpu().numpy()
+            entropy, kl = -vals[0], vals[1]
+            numeric_error, kl_numeric_error = bool(vals[2]), bool(vals[3])
+        else:
+            loss, numeric_error = fns.policy_update(optimizer, behavioral_policy, target_policy,
+                                                    states, actions, num_traj, real_traj_lengths,
+                                                    distances, indices, k, G, B, ns, eps)
+            entropy = -_np(loss)
+            kl, kl_numeric_error = fns.compute_kl(behavioral_policy, target_policy, states,
+                                                  actions, num_traj, real_traj_lengths,
+                                                  distances, indices, k, eps)
+            kl = _np(kl)
 
         if not numeric_error and not kl_numeric_error and kl <= kl_threshold:
-            last_valid_target_policy.load_state_dict(target_policy.state_dict())
+            _copy_policy(last_valid_target_policy, target_policy)
             num_off_iters += 1
             if on_accept is not None:
                 on_accept(num_off_iters, entropy, kl, learning_rate)
         else:
             if use_backtracking:
                 if not backtrack_iter == max_backtrack_try:
-                    target_policy.load_state_dict(last_valid_target_policy.state_dict())
+                    _copy_policy(target_policy, last_valid_target_policy)
                     learning_rate = original_lr / (backtrack_coeff ** backtrack_iter)
                     for param_group in optimizer.param_groups:
                         param_group["lr"] = learning_rate
@@ -514,6 +550,19 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
                                       actions, num_traj, real_traj_lengths, distances, indices, k,
                                       G, B, ns, eps)
     return entropy, num_off_iters, backtrack_iter, learning_rate
+
+
+_BUILTIN_STEP_FNS = (policy_update, compute_kl)
+
+
+def _copy_policy(dst, src):
+    """dst.load_state_dict(src.state_dict()) (mepol.py:443,456) as one fused device copy."""
+    dp, sp = list(dst.parameters()), list(src.parameters())
+    if len(dp) != len(sp) or list(dst.buffers()) or list(src.buffers()):
+        dst.load_state_dict(src.state_dict())
+        return
+    with torch.no_grad():
+        torch._foreach_copy_(dp, sp)
 
 
 def _np(x):

@@ -123,7 +123,7 @@ class ShardedEpoch:
         lt, lb = self._logps(beh, tgt)
         return _ShardedEntropy.apply(lt, lb, self, k, G, B, ns, eps)
 
-    def compute_kl(self, beh, tgt, k, eps):
+    def compute_kl_deferred(self, beh, tgt, k, eps):
         from .algorithms.particles import _param_key
 
         lb = self.behavioral_logp(beh)
@@ -139,8 +139,11 @@ class ShardedEpoch:
             _, wg = self.weights(lt, lb)
             _, KL, _ = self.entropy_sums(wg, k, 1.0, 0.0, 1.0, eps)
         kl = KL.clone()
-        numeric_error = bool(torch.isinf(kl) or torch.isnan(kl))
-        return torch.clamp_min(kl, 0.0), numeric_error
+        return torch.clamp_min(kl, 0.0), ~torch.isfinite(kl)
+
+    def compute_kl(self, beh, tgt, k, eps):
+        kl, flag = self.compute_kl_deferred(beh, tgt, k, eps)
+        return kl, bool(flag)
 
     def allreduce_grads(self, params):
         grads = [p.grad for p in params if p.grad is not None]
@@ -154,14 +157,18 @@ class ShardedEpoch:
             g.copy_(flat[o:o + n].view_as(g))
             o += n
 
-    def policy_update(self, optimizer, beh, tgt, k, G, B, ns, eps):
+    def policy_update_deferred(self, optimizer, beh, tgt, k, G, B, ns, eps):
         optimizer.zero_grad()
         loss = -self.compute_entropy(beh, tgt, k, G, B, ns, eps)
-        numeric_error = bool(torch.isinf(loss) or torch.isnan(loss))
+        flag = ~torch.isfinite(loss.detach())
         loss.backward()
         self.allreduce_grads(list(tgt.parameters()))
         optimizer.step()
-        return loss, numeric_error
+        return loss, flag
+
+    def policy_update(self, optimizer, beh, tgt, k, G, B, ns, eps):
+        loss, flag = self.policy_update_deferred(optimizer, beh, tgt, k, G, B, ns, eps)
+        return loss, bool(flag)
 
     def off_policy_optimization(self, optimizer, beh, tgt, last_valid, G, B, ns, eps,
                                 kl_threshold, max_off_iters, use_backtracking, backtrack_coeff,
@@ -178,6 +185,14 @@ class ShardedEpoch:
             @staticmethod
             def compute_kl(b, t, *a):
                 return self.compute_kl(b, t, k, eps)
+
+            @staticmethod
+            def policy_update_deferred(opt, b, t, *a):
+                return self.policy_update_deferred(opt, b, t, k, G, B, ns, eps)
+
+            @staticmethod
+            def compute_kl_deferred(b, t, *a):
+                return self.compute_kl_deferred(b, t, k, eps)
 
             @staticmethod
             def compute_entropy(b, t, *a):
