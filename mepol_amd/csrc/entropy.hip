@@ -181,7 +181,16 @@ __global__ __launch_bounds__(256) void gamma_kernel(const double* __restrict__ g
   if (j < n) {
     double gj = 0.0;
     const int32_t b = off[j], e = off[j + 1];
-    for (int32_t x = b; x < e; ++x) gj += g[rows[x]];
+    // Eight gathers in flight per step; the sum stays in CSR order (sequential, as one loop).
+    constexpr int kU = 8;
+    for (int32_t x = b; x < e; x += kU) {
+      double v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) v[u] = g[rows[min(x + u, e - 1)]];
+#pragma unroll
+      for (int u = 0; u < kU; ++u)
+        if (x + u < e) gj += v[u];
+    }
     gamma[j] = gj;
     s = gj * w[j];
   }

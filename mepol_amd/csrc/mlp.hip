@@ -15,26 +15,27 @@ namespace mepol {
 namespace mlp {
 
 constexpr int kChunk = 64;  // rows staged per block iteration
+constexpr int kThreads = 256;
 
 // Stage kChunk rows of x (contiguous kChunk*F doubles) into LDS with coalesced loads; features
-// [F, FP) stay zero so the unrolled FMA chain needs no per-feature guard.
+// [F, FP) stay zero so the unrolled FMA chain needs no per-feature guard.  Several blocks per CU
+// overlap one block's staging with the others' compute.
 template <int FP>
-__device__ __forceinline__ int stage_rows(const double* __restrict__ x, int64_t N, int F,
-                                          int64_t r0, double (*sx)[FP]) {
-  const int nrow = (int)min<int64_t>(kChunk, N - r0);
+__device__ __forceinline__ void stage_rows(const double* __restrict__ x, int F, int nrow,
+                                           int64_t r0, double (*sx)[FP]) {
   const double* src = x + r0 * F;
-  for (int e = threadIdx.x; e < nrow * F; e += blockDim.x) {
+  for (int e = threadIdx.x; e < nrow * F; e += kThreads) {
     const int rr = e / F;
     sx[rr][e - rr * F] = src[e];
   }
-  return nrow;
 }
 
 template <int FP>
-__global__ __launch_bounds__(256) void layer_fwd_kernel(const double* __restrict__ x, int64_t N,
-                                                        int F, const double* __restrict__ W,
-                                                        const double* __restrict__ b, int H,
-                                                        double* __restrict__ h) {
+__global__ __launch_bounds__(kThreads) void layer_fwd_kernel(const double* __restrict__ x,
+                                                             int64_t N, int F,
+                                                             const double* __restrict__ W,
+                                                             const double* __restrict__ b, int H,
+                                                             double* __restrict__ h) {
   __shared__ double sx[kChunk][FP];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + l;
@@ -43,11 +44,14 @@ __global__ __launch_bounds__(256) void layer_fwd_kernel(const double* __restrict
 #pragma unroll
   for (int f = 0; f < FP; ++f) wr[f] = (col && f < F) ? W[(int64_t)c * F + f] : 0.0;
   const double bc = col ? b[c] : 0.0;
-  for (int e = threadIdx.x; e < kChunk * FP; e += blockDim.x) sx[e / FP][e % FP] = 0.0;
-  for (int64_t r0 = (int64_t)blockIdx.x * kChunk; r0 < N; r0 += (int64_t)gridDim.x * kChunk) {
+  for (int e = threadIdx.x; e < kChunk * FP; e += kThreads) sx[e / FP][e % FP] = 0.0;
+  const int64_t step = (int64_t)gridDim.x * kChunk;
+  for (int64_t r0 = (int64_t)blockIdx.x * kChunk; r0 < N; r0 += step) {
+    const int nrow = (int)min<int64_t>(kChunk, N - r0);
     __syncthreads();
-    const int nrow = stage_rows<FP>(x, N, F, r0, sx);
+    stage_rows<FP>(x, F, nrow, r0, sx);
     __syncthreads();
+#pragma unroll 1
     for (int rr = w; rr < nrow; rr += 4) {
       double acc = bc;
 #pragma unroll
@@ -59,33 +63,45 @@ __global__ __launch_bounds__(256) void layer_fwd_kernel(const double* __restrict
 
 // part: [gridDim.x][H][F + 1]  (dW row c then db_c)
 template <int FP>
-__global__ __launch_bounds__(256) void layer_bwd_kernel(const double* __restrict__ dh,
-                                                        const double* __restrict__ h,
-                                                        const double* __restrict__ x, int64_t N,
-                                                        int F, int H, double* __restrict__ part) {
+__global__ __launch_bounds__(kThreads) void layer_bwd_kernel(const double* __restrict__ dh,
+                                                             const double* __restrict__ h,
+                                                             const double* __restrict__ x,
+                                                             int64_t N, int F, int H,
+                                                             double* __restrict__ part) {
+  constexpr int kRows = 4;  // rows of h/dh in flight per wave
   __shared__ double sx[kChunk][FP];
   __shared__ double sacc[64][FP + 1];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.y * 64 + l;
   const bool col = c < H;
+  const int cc = col ? c : H - 1;  // clamped column: loads stay in bounds, results discarded
   double acc[FP], accb = 0.0;
 #pragma unroll
   for (int f = 0; f < FP; ++f) acc[f] = 0.0;
-  for (int e = threadIdx.x; e < kChunk * FP; e += blockDim.x) sx[e / FP][e % FP] = 0.0;
-  for (int64_t r0 = (int64_t)blockIdx.x * kChunk; r0 < N; r0 += (int64_t)gridDim.x * kChunk) {
+  for (int e = threadIdx.x; e < kChunk * FP; e += kThreads) sx[e / FP][e % FP] = 0.0;
+  const int64_t step = (int64_t)gridDim.x * kChunk;
+  for (int64_t r0 = (int64_t)blockIdx.x * kChunk; r0 < N; r0 += step) {
+    const int nrow = (int)min<int64_t>(kChunk, N - r0);
     __syncthreads();
-    const int nrow = stage_rows<FP>(x, N, F, r0, sx);
+    stage_rows<FP>(x, F, nrow, r0, sx);
     __syncthreads();
-    for (int rr = w; rr < nrow; rr += 4) {
-      double dz = 0.0;
-      if (col) {
-        const int64_t o = (r0 + rr) * H + c;
-        const double hv = h[o];
-        dz = (hv > 0.0) ? dh[o] : 0.0;
+#pragma unroll 1
+    for (int rb = w * kRows; rb < nrow; rb += 4 * kRows) {
+      double hv[kRows], dv[kRows];
+#pragma unroll
+      for (int q = 0; q < kRows; ++q) {
+        const int rr = min(rb + q, nrow - 1);
+        const int64_t o = (r0 + rr) * H + cc;
+        hv[q] = h[o];
+        dv[q] = dh[o];
       }
 #pragma unroll
-      for (int f = 0; f < FP; ++f) acc[f] = fma(dz, sx[rr][f], acc[f]);
-      accb += dz;
+      for (int q = 0; q < kRows; ++q) {
+        const double dz = (col && rb + q < nrow && hv[q] > 0.0) ? dv[q] : 0.0;
+#pragma unroll
+        for (int f = 0; f < FP; ++f) acc[f] = fma(dz, sx[min(rb + q, kChunk - 1)][f], acc[f]);
+        accb += dz;
+      }
     }
   }
   // Fixed-order cross-wave sum: wave 0 writes, waves 1..3 add in turn.
@@ -119,7 +135,22 @@ __global__ void layer_reduce_kernel(const double* __restrict__ part, int nb, int
     db[c] = s;
 }
 
-constexpr int kRowBlocks = 256;  // row-chunk blocks per column tile (grid-stride over chunks)
+constexpr int kRowBlocks = 256;  // upper bound on row-chunk blocks per column tile
+
+// Blocks per column tile so that the whole grid is resident at once (no partial second wave of
+// blocks): CUs x resident blocks per CU / column tiles, capped by kRowBlocks and the chunks.
+template <typename Kernel>
+int row_blocks(Kernel kernel, int64_t n, int col_tiles) {
+  int dev = 0, cus = 256, per_cu = 1;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess ||
+      per_cu < 1)
+    per_cu = 1;
+  const int64_t chunks = std::max<int64_t>((n + kChunk - 1) / kChunk, 1);
+  const int64_t fit = std::max<int64_t>((int64_t)cus * per_cu / col_tiles, 1);
+  return (int)std::min<int64_t>(std::min<int64_t>(fit, kRowBlocks), chunks);
+}
 
 }  // namespace mlp
 }  // namespace mepol
@@ -157,11 +188,13 @@ extern "C" int mepol_layer_forward(const double* x, int64_t n, int in_features, 
     return kErrBadArg;
   }
   if (n == 0) return 0;
-  const int gx = (int)std::min<int64_t>(kRowBlocks, (n + kChunk - 1) / kChunk);
-  dim3 g(gx, (out_features + 63) / 64);
+  const int gy = (out_features + 63) / 64;
   hipStream_t st = (hipStream_t)stream;
-  MEPOL_FP_SWITCH(in_features, hipLaunchKernelGGL((layer_fwd_kernel<FP>), g, dim3(256), 0, st, x,
-                                                  n, in_features, W, b, out_features, h_out));
+  MEPOL_FP_SWITCH(in_features, {
+    const int gx = row_blocks(layer_fwd_kernel<FP>, n, gy);
+    hipLaunchKernelGGL((layer_fwd_kernel<FP>), dim3(gx, gy), dim3(kThreads), 0, st, x, n,
+                       in_features, W, b, out_features, h_out);
+  });
   MEPOL_CHECK_LAUNCH();
   return 0;
 }
@@ -183,17 +216,19 @@ extern "C" int mepol_layer_backward(const double* dh, const double* h, const dou
     set_error("mepol_layer_backward: bad arguments");
     return kErrBadArg;
   }
-  const int gx = (int)std::min<int64_t>(kRowBlocks, (n + kChunk - 1) / kChunk);
+  const int gy = (out_features + 63) / 64;
+  int gx = 1;
+  MEPOL_FP_SWITCH(in_features, gx = row_blocks(layer_bwd_kernel<FP>, n, gy));
   const size_t need = (size_t)gx * out_features * (in_features + 1) * sizeof(double);
   if (workspace_bytes < need) {
     set_error("mepol_layer_backward: workspace %zu < %zu", workspace_bytes, need);
     return kErrWorkspace;
   }
   hipStream_t st = (hipStream_t)stream;
-  dim3 g(gx, (out_features + 63) / 64);
   double* part = (double*)workspace;
-  MEPOL_FP_SWITCH(in_features, hipLaunchKernelGGL((layer_bwd_kernel<FP>), g, dim3(256), 0, st, dh,
-                                                  h, x, n, in_features, out_features, part));
+  MEPOL_FP_SWITCH(in_features,
+                  hipLaunchKernelGGL((layer_bwd_kernel<FP>), dim3(gx, gy), dim3(kThreads), 0, st,
+                                     dh, h, x, n, in_features, out_features, part));
   MEPOL_CHECK_LAUNCH();
   const int64_t m = (int64_t)out_features * (in_features + 1);
   hipLaunchKernelGGL(layer_reduce_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, part,
