@@ -1,0 +1,42 @@
+"""HBM bytes per k-NN call from the two rocprofv3 --pmc passes of tools/knn_pmc.sh.
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  Per MI355X_MICROARCH.md (HBM section) FETCH_SIZE
+is doubled on gfx950 (it tallies 128-B requests at 64 B); WRITE_SIZE is taken as reported.
+The k-NN call is pack + select + refine (+ exact fallback); the last call of the run is used.
+Writes profiles/knn_pmc.json (read by bench.py for roofline.traffic).
+"""
+import json
+import os
+import sqlite3
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_call(db, counter):
+    c = sqlite3.connect(db)
+    rows = c.execute("select dispatch_id, kernel_name, value from counters_collection "
+                     "where counter_name=? order by dispatch_id", (counter,)).fetchall()
+    knn = [(d, n, v) for d, n, v in rows if "mepol::knn::" in n]
+    # A call starts at each pack kernel; keep the last call.
+    starts = [i for i, (_, n, _) in enumerate(knn) if "pack_kernel" in n]
+    last = knn[starts[-1]:]
+    return {n.split("(")[0]: v * 1024.0 for _, n, v in last}
+
+
+def main(src="gpurun_out"):
+    fetch = per_call(os.path.join(src, "pmc_FETCH_SIZE", "run_results.db"), "FETCH_SIZE")
+    write = per_call(os.path.join(src, "pmc_WRITE_SIZE", "run_results.db"), "WRITE_SIZE")
+    kernels = {k: {"fetch_bytes_raw": fetch.get(k), "fetch_bytes_x2": 2 * fetch.get(k, 0.0),
+                   "write_bytes": write.get(k)} for k in sorted(set(fetch) | set(write))}
+    total = sum(2 * v for v in fetch.values()) + sum(write.values())
+    out = {"hbm_bytes_per_launch": total, "kernels": kernels,
+           "workload": "C3 k-NN: N=200000 queries x 200000 candidates, d=29, k+1=31",
+           "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KiB -> bytes"}
+    path = os.path.join(ROOT, "profiles", "knn_pmc.json")
+    json.dump(out, open(path, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
