@@ -138,6 +138,16 @@ int mepol_rollout_step(int env_id, double* env_f64, float* env_f32, const double
                        int64_t T, float* states_rec, float* actions_rec, double* policy_in,
                        void* stream);
 
+/* ---- Optimizer step of policy_update (mepol.py:280, optimizer.step()) ------------------------
+ * Replaces torch.optim.Adam(lr).step() (kind 0) / torch.optim.RMSprop(lr).step() (kind 1) as
+ * constructed at mepol.py:308-311, over n_tensors (<= 8) f64 parameter tensors in one launch.
+ * exp_avg (Adam only) / exp_avg_sq (Adam; RMSprop square_avg) are updated in place.
+ * scalars is DEVICE memory: Adam {enable, lr/bias_correction1, sqrt(bias_correction2), beta1,
+ * beta2, eps}; RMSprop {enable, lr, alpha, eps}.  enable == 0 makes the call a no-op. */
+int mepol_optim_step(int kind, int n_tensors, double* const* params, const double* const* grads,
+                     double* const* exp_avg, double* const* exp_avg_sq, const int64_t* sizes,
+                     const double* scalars, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,279 @@
+"""One off-policy iteration of MEPOL as a replayable HIP graph.
+
+An iteration of the reference's loop (src/algorithms/mepol.py:429-439) is
+``policy_update`` (entropy at theta_t, backward, optimizer step) followed by ``compute_kl``
+(KL at theta_t+1).  For the reference's two-hidden-layer ReLU policy that whole sequence is a
+fixed list of device launches:
+
+    iw_forward -> entropy_forward -> entropy_gamma -> entropy_reverse_scan      (dH/dlogp)
+    head_backward -> split-K dW2 -> dh1 GEMM -> layer_backward                 (dH/dtheta)
+    optim_step (Adam / RMSprop)                                                (theta_t+1)
+    layer_forward -> GEMM -> head_forward                                      (logp at t+1)
+    iw_forward -> entropy_forward                                              (KL at t+1)
+
+The forward at theta_t+1 is written into static buffers that the next replay's backward reads,
+so one captured graph replays every iteration and the host only reads the two control scalars
+(H, KL) per iteration.  The Adam/RMSprop state lives in the caller's torch optimizer
+(``optimizer.state[p]``: ``step``, ``exp_avg``, ``exp_avg_sq`` / ``square_avg``), updated in
+place; its per-step scalars (bias corrections, learning rate) are written to a device buffer
+before each replay.  After a rejected step the caller restores theta and calls ``refresh()``.
+
+Results equal the eager path (autograd through the same kernels) up to the optimizer's
+rounding order; tests/test_gpu_device_loop.py checks both against each other and the oracle.
+"""
+import math
+import os
+import weakref
+
+import torch
+import torch.nn as nn
+
+from .. import ops
+from ..policy import GaussianPolicy, _weight_grad
+
+_ADAM, _RMSPROP = 0, 1
+
+
+def _opt_kind(optimizer):
+    if len(optimizer.param_groups) != 1:
+        return None
+    g = optimizer.param_groups[0]
+    if isinstance(g.get("lr"), torch.Tensor) or g.get("weight_decay", 0) != 0 or g.get(
+            "maximize", False) or g.get("differentiable", False) or g.get(
+            "capturable", False) or g.get("fused", False):
+        return None
+    if type(optimizer) is torch.optim.Adam:
+        if g.get("amsgrad", False) or g.get("decoupled_weight_decay", False):
+            return None
+        return _ADAM
+    if type(optimizer) is torch.optim.RMSprop:
+        if g.get("momentum", 0) != 0 or g.get("centered", False):
+            return None
+        return _RMSPROP
+    return None
+
+
+def supported(batch, behavioral_policy, target_policy, optimizer):
+    """True when the iteration can run as a graph: the reference's 2-layer ReLU GaussianPolicy
+    (f64, fused-head sizes), a dense particle grid, Adam/RMSprop with MEPOL's settings over
+    exactly the target's parameters."""
+    if os.environ.get("MEPOL_DEVICE_LOOP", "1") == "0":
+        return False
+    if not isinstance(target_policy, GaussianPolicy) or target_policy is behavioral_policy:
+        return False
+    if not (batch.dense and batch.states_flat.is_cuda):
+        return False
+    if not target_policy._fused_head_ok(batch.states_flat, batch.actions_flat):
+        return False
+    layers = [m for m in target_policy.net if isinstance(m, nn.Linear)]
+    if len(layers) != 2 or target_policy.num_features > 64:
+        return False
+    params = list(target_policy.parameters())
+    if len(params) != 7 or any(p.dtype != torch.float64 or not p.is_contiguous() or
+                               p.device != batch.device for p in params):
+        return False
+    if _opt_kind(optimizer) is None:
+        return False
+    return [id(p) for p in optimizer.param_groups[0]["params"]] == [id(p) for p in params]
+
+
+def _scalar_dtype():
+    try:
+        from torch.optim.optimizer import _get_scalar_dtype
+
+        return _get_scalar_dtype()
+    except ImportError:  # pragma: no cover
+        return torch.float32
+
+
+class DeviceIteration:
+    """Static buffers + captured graph for one (policy, optimizer, batch shape, k, constants)."""
+
+    def __init__(self, target_policy, optimizer, batch, k, G, B, ns, eps):
+        self.tgt, self.opt = target_policy, optimizer
+        self.kind = _opt_kind(optimizer)
+        self.params = list(target_policy.parameters())  # optimizer / state order
+        l1, l2 = [m for m in target_policy.net if isinstance(m, nn.Linear)]
+        self.named = (l1.weight, l1.bias, l2.weight, l2.bias, target_policy.mean.weight,
+                      target_policy.mean.bias, target_policy.log_std)
+        self.k, self.G, self.B, self.ns, self.eps = k, float(G), float(B), float(ns), float(eps)
+        dev = batch.device
+        self.device = dev
+        self.N, self.nt, self.T, self.kp1 = batch.N, batch.num_traj, batch.T, batch.kp1
+        W1, _, W2, _, Wm, _, _ = self.named
+        f64 = dict(dtype=torch.float64, device=dev)
+        self.x = torch.empty_like(batch.states_flat)
+        self.act = torch.empty_like(batch.actions_flat)
+        self.D = torch.empty_like(batch.D)
+        self.idx32T = torch.empty_like(batch.idx32T)
+        self.offsets = torch.empty_like(batch.offsets)
+        self.logp_b = torch.empty((self.nt, self.T), **f64)
+        off, rows = batch.csr(k)
+        self.csr_off, self.csr_rows = torch.empty_like(off), torch.empty_like(rows)
+        self.h1 = torch.empty((self.N, W1.shape[0]), **f64)
+        self.z2 = torch.empty((self.N, W2.shape[0]), **f64)
+        self.mu = torch.empty((self.N, Wm.shape[0]), **f64)
+        self.logp = torch.empty(self.N, **f64)
+        self.neg_one = torch.full((), -1.0, **f64)
+        self.scal = torch.zeros(8, **f64)
+        self.scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
+        self.vals = torch.zeros(2, **f64)
+        self.graph = None
+        self._batch_id = None
+        self._init_state()
+
+    def matches(self, target_policy, optimizer, batch, k, G, B, ns, eps):
+        return (target_policy is self.tgt and optimizer is self.opt and batch.N == self.N
+                and batch.num_traj == self.nt and batch.T == self.T and batch.kp1 == self.kp1
+                and batch.device == self.device and (k, float(G), float(B), float(ns), float(eps))
+                == (self.k, self.G, self.B, self.ns, self.eps)
+                and batch.states_flat.shape == self.x.shape
+                and batch.actions_flat.shape == self.act.shape
+                and [p.data_ptr() for p in target_policy.parameters()]
+                == [p.data_ptr() for p in self.params])
+
+    # -- optimizer state (kept in the torch optimizer, as torch.optim would) ------------------
+    def _init_state(self):
+        for p in self.params:
+            st = self.opt.state[p]
+            if "step" not in st:
+                st["step"] = torch.tensor(0.0, dtype=_scalar_dtype())
+                if self.kind == _ADAM:
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                else:
+                    st["square_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        if self.kind == _ADAM:
+            self.m = [self.opt.state[p]["exp_avg"] for p in self.params]
+            self.v = [self.opt.state[p]["exp_avg_sq"] for p in self.params]
+        else:
+            self.m = None
+            self.v = [self.opt.state[p]["square_avg"] for p in self.params]
+        for t in (self.m or []) + self.v:
+            if t.dtype != torch.float64 or not t.is_contiguous() or t.device != self.device:
+                raise ValueError("optimizer state is not contiguous f64 on the policy's device")
+
+    def _state_tensors_current(self):
+        st = self.opt.state
+        if self.kind == _ADAM:
+            return all(st[p].get("exp_avg") is m and st[p].get("exp_avg_sq") is v
+                       for p, m, v in zip(self.params, self.m, self.v))
+        return all(st[p].get("square_avg") is v for p, v in zip(self.params, self.v))
+
+    def _advance_scalars(self):
+        """torch.optim's host-side step bookkeeping for one step; returns the device scalars."""
+        g = self.opt.param_groups[0]
+        steps = [self.opt.state[p]["step"] for p in self.params]
+        for s in steps:
+            s += 1
+        lr = g["lr"]
+        h = self.scal_host
+        h[0] = 1.0
+        if self.kind == _ADAM:
+            beta1, beta2 = g["betas"]
+            step = float(steps[0])
+            bc1 = 1 - beta1 ** step
+            bc2 = 1 - beta2 ** step
+            h[1] = lr / bc1
+            h[2] = bc2 ** 0.5
+            h[3], h[4], h[5] = beta1, beta2, g["eps"]
+        else:
+            h[1], h[2], h[3] = lr, g["alpha"], g["eps"]
+
+    # -- the iteration --------------------------------------------------------------------------
+    def load(self, batch, logp_b):
+        """Copy one epoch's particles and cached per-epoch tensors into the static inputs."""
+        off, rows = batch.csr(self.k)
+        for dst, src in ((self.x, batch.states_flat), (self.act, batch.actions_flat),
+                         (self.D, batch.D), (self.idx32T, batch.idx32T),
+                         (self.offsets, batch.offsets), (self.logp_b, logp_b),
+                         (self.csr_off, off), (self.csr_rows, rows)):
+            dst.copy_(src)
+        self._batch_id = id(batch)
+
+    @torch.no_grad()
+    def forward(self):
+        """logp of the target at its current parameters into the static buffers."""
+        W1, b1, W2, b2, Wm, bm, ls = self.named
+        ops.layer_forward(self.x, W1, b1, out=self.h1)
+        torch.mm(self.h1, W2.t(), out=self.z2)
+        ops.head_forward(self.z2, Wm, bm, ls, self.act, bz=b2, mu_out=self.mu, logp_out=self.logp)
+
+    refresh = forward
+
+    @torch.no_grad()
+    def _body(self):
+        W1, b1, W2, b2, Wm, bm, ls = self.named
+        nt, T, N, k = self.nt, self.T, self.N, self.k
+        lt = self.logp.view(nt, T)
+        # entropy at theta_t and dH/dlogp (compute_entropy + loss.backward, mepol.py:273-278)
+        _, _, w, _ = ops.iw_forward(lt, self.logp_b, self.offsets, N)
+        out_h, _, g = ops.entropy_forward(w, self.idx32T, self.D, k, self.ns, self.G, self.B,
+                                          self.eps)
+        gamma, partials, nparts = ops.entropy_gamma(g, w, self.csr_off, self.csr_rows)
+        grad = ops.entropy_reverse_scan(gamma, w, partials, nparts, self.offsets, nt, T,
+                                        self.neg_one)
+        # through the policy (the _TwoLayerLogp backward)
+        dz2, dWm, dbm, dls, db2 = ops.head_backward(grad.view(-1), self.z2, Wm, ls, self.act,
+                                                    self.mu, bz=b2, need_dz=True)
+        dW2 = _weight_grad(dz2, self.h1)
+        dh1 = torch.mm(dz2, W2)
+        dW1, db1 = ops.layer_backward(dh1, self.h1, self.x)
+        # optimizer.step() (mepol.py:280)
+        grad_of = {id(p): g for p, g in zip(self.named, (dW1, db1, dW2, db2, dWm, dbm, dls))}
+        ops.optim_step(self.kind, self.params, [grad_of[id(p)] for p in self.params], self.m,
+                       self.v, self.scal)
+        # compute_kl at theta_t+1 (mepol.py:435, :157-174)
+        self.forward()
+        _, _, w2, _ = ops.iw_forward(lt, self.logp_b, self.offsets, N)
+        out_k, _, _ = ops.entropy_forward(w2, self.idx32T, self.D, k, 1.0, 1.0, 0.0, self.eps)
+        torch.cat((out_h[:1], out_k[1:2]), out=self.vals)
+
+    def _capture(self):
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream(device=self.device)
+        self.scal.zero_()  # enable = 0: the warm-up pass leaves theta and the moments untouched
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):
+            self._body()
+        cur.wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=side):
+            self._body()
+        cur.wait_stream(side)
+        self.graph = graph
+
+    def step(self):
+        """policy_update + compute_kl.  Returns host floats (H(theta_t), KL(theta_t+1)
+        unclamped); the target policy's parameters and the optimizer state are updated."""
+        if not self._state_tensors_current():
+            self._init_state()
+            self.graph = None
+        if self.graph is None:
+            self._capture()
+        self._advance_scalars()
+        self.scal.copy_(self.scal_host, non_blocking=True)
+        self.graph.replay()
+        v = self.vals.cpu()
+        return float(v[0]), float(v[1])
+
+
+_CACHE = weakref.WeakKeyDictionary()  # target policy -> DeviceIteration
+
+
+def get(target_policy, optimizer, batch, k, G, B, ns, eps):
+    """The cached DeviceIteration for these arguments (one per target policy)."""
+    it = _CACHE.get(target_policy)
+    if it is None or not it.matches(target_policy, optimizer, batch, k, G, B, ns, eps):
+        it = None  # drop the old graph and buffers before allocating new ones
+        _CACHE.pop(target_policy, None)
+        it = DeviceIteration(target_policy, optimizer, batch, k, G, B, ns, eps)
+        _CACHE[target_policy] = it
+    return it
+
+
+def kl_flags(H, KL):
+    """(loss, loss_numeric_error, kl (clamped as torch.clamp_min), kl_numeric_error)."""
+    loss = -H
+    kl = KL if not (KL < 0.0) else 0.0
+    return loss, not math.isfinite(loss), kl, not math.isfinite(KL)

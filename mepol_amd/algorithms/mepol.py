@@ -500,8 +500,22 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
         # A caller that replaced policy_update / compute_kl (reference-style patching) gets
         # its functions called, not the deferred built-ins.
         deferred = (fns.policy_update, fns.compute_kl) == _BUILTIN_STEP_FNS
+    loop = None
+    if deferred and fns is sys.modules[__name__]:
+        from . import device_loop
+
+        batch = P.lookup(states, actions, real_traj_lengths, distances, indices)
+        if device_loop.supported(batch, behavioral_policy, target_policy, optimizer):
+            loop = device_loop.get(target_policy, optimizer, batch, k, G, B, ns, eps)
+            loop.load(batch, batch.behavioral_logp(behavioral_policy))
+            loop.refresh()
     while not kl_threshold_reached:
-        if deferred:
+        if loop is not None:
+            # policy_update + compute_kl as one graph replay; two scalars come back
+            H, KL = loop.step()
+            loss, numeric_error, kl, kl_numeric_error = device_loop.kl_flags(H, KL)
+            entropy = -loss
+        elif deferred:
             # Queue the update and the KL pass, then read all four control scalars at once.
             loss, loss_flag = fns.policy_update_deferred(
                 optimizer, behavioral_policy, target_policy, states, actions, num_traj,
@@ -533,6 +547,8 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
             if use_backtracking:
                 if not backtrack_iter == max_backtrack_try:
                     _copy_policy(target_policy, last_valid_target_policy)
+                    if loop is not None:
+                        loop.refresh()
                     learning_rate = original_lr / (backtrack_coeff ** backtrack_iter)
                     for param_group in optimizer.param_groups:
                         param_group["lr"] = learning_rate

@@ -10,6 +10,9 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <map>
+#include <mutex>
+#include <utility>
 
 namespace mepol {
 namespace mlp {
@@ -139,16 +142,32 @@ constexpr int kRowBlocks = 256;  // upper bound on row-chunk blocks per column t
 
 // Blocks per column tile so that the whole grid is resident at once (no partial second wave of
 // blocks): CUs x resident blocks per CU / column tiles, capped by kRowBlocks and the chunks.
+// The device queries are cached (first call per kernel/device), so launches made under HIP
+// graph capture issue no runtime queries.
 template <typename Kernel>
 int row_blocks(Kernel kernel, int64_t n, int col_tiles) {
-  int dev = 0, cus = 256, per_cu = 1;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) != hipSuccess ||
-      per_cu < 1)
-    per_cu = 1;
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, int> cache;  // (kernel, device) -> CUs x blocks
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  int resident;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    auto key = std::make_pair((const void*)kernel, dev);
+    auto it = cache.find(key);
+    if (it == cache.end()) {
+      int cus = 256, per_cu = 1;
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kThreads, 0) !=
+              hipSuccess ||
+          per_cu < 1)
+        per_cu = 1;
+      it = cache.emplace(key, cus * per_cu).first;
+    }
+    resident = it->second;
+  }
   const int64_t chunks = std::max<int64_t>((n + kChunk - 1) / kChunk, 1);
-  const int64_t fit = std::max<int64_t>((int64_t)cus * per_cu / col_tiles, 1);
+  const int64_t fit = std::max<int64_t>((int64_t)resident / col_tiles, 1);
   return (int)std::min<int64_t>(std::min<int64_t>(fit, kRowBlocks), chunks);
 }
 

@@ -185,12 +185,13 @@ def entropy_reverse_scan(gamma, w, partials, nparts, offsets, nt, T_stride, grad
     return grad
 
 
-def head_forward(z, Wm, bm, log_std, act, bz=None):
+def head_forward(z, Wm, bm, log_std, act, bz=None, mu_out=None, logp_out=None):
     """Fused Gaussian head: (mu [n, a], logp [n]) from the last pre-activation z (+ bias bz)."""
     n, h = z.shape
     a = Wm.shape[0]
-    mu = torch.empty((n, a), dtype=torch.float64, device=z.device)
-    logp = torch.empty(n, dtype=torch.float64, device=z.device)
+    mu = mu_out if mu_out is not None else torch.empty((n, a), dtype=torch.float64, device=z.device)
+    logp = logp_out if logp_out is not None else torch.empty(n, dtype=torch.float64,
+                                                             device=z.device)
     call("mepol_head_forward", ptr(z), n, h, ptr(bz), ptr(Wm), ptr(bm), ptr(log_std), ptr(act), a,
          ptr(mu), ptr(logp), _stream())
     return mu, logp
@@ -217,10 +218,11 @@ def head_backward(grad_logp, z, Wm, log_std, act, mu, bz=None, need_dz=True):
     return dz, dWm, dbm, dls, dbz
 
 
-def layer_forward(x, W, b):
+def layer_forward(x, W, b, out=None):
     """h = relu(x W^T + b) for the policy's input layer (in_features <= 64)."""
     n, f = x.shape
-    h = torch.empty((n, W.shape[0]), dtype=torch.float64, device=x.device)
+    h = out if out is not None else torch.empty((n, W.shape[0]), dtype=torch.float64,
+                                                device=x.device)
     call("mepol_layer_forward", ptr(x), n, f, ptr(W), ptr(b), W.shape[0], ptr(h), _stream())
     return h
 
@@ -239,6 +241,23 @@ def layer_backward(dh, h, x):
     call("mepol_layer_backward", ptr(dh), ptr(h), ptr(x), n, f, out, ptr(dW), ptr(db), ptr(ws),
          ws.numel(), _stream())
     return dW, db
+
+
+def optim_step(kind, params, grads, exp_avg, exp_avg_sq, scalars):
+    """In-place Adam (kind 0) / RMSprop (kind 1) update of f64 tensors; scalars is a device f64
+    tensor (see include/mepol_amd.h, mepol_optim_step)."""
+    import ctypes
+
+    n = len(params)
+    arr = ctypes.c_void_p * n
+    for t in list(params) + list(grads) + list(exp_avg_sq) + list(exp_avg or []):
+        if t.dtype != torch.float64 or not t.is_contiguous() or not t.is_cuda:
+            raise ValueError("optim_step needs contiguous f64 device tensors")
+    sizes = (ctypes.c_int64 * n)(*[t.numel() for t in params])
+    m = arr(*[t.data_ptr() for t in exp_avg]) if exp_avg is not None else None
+    call("mepol_optim_step", kind, n, arr(*[t.data_ptr() for t in params]),
+         arr(*[t.data_ptr() for t in grads]), m, arr(*[t.data_ptr() for t in exp_avg_sq]),
+         sizes, ptr(scalars), _stream())
 
 
 def step_mountaincar(state, action):

@@ -1,0 +1,105 @@
+"""The graph-replayed off-policy iteration (algorithms/device_loop.py) == the eager path
+(autograd through the same kernels) == the oracle's torch CPU loop, with Adam and RMSprop,
+with and without backtracking (mepol.py:416-483)."""
+import copy
+
+import numpy as np
+import pytest
+import scipy.special
+import torch
+
+pytestmark = pytest.mark.gpu
+
+NT, T, NF, A, K, HID = 16, 1250, 29, 8, 10, [64, 48]  # N = 20000 >= the fused-path minimum
+
+
+def _setup(opt_name, lr, seed=5):
+    from mepol_amd.algorithms import mepol as M
+    from mepol_amd.policy import GaussianPolicy
+
+    rng = np.random.default_rng(seed)
+    states = rng.standard_normal((NT, T + 1, NF)).astype(np.float32)
+    actions = (0.5 * rng.standard_normal((NT, T, A))).astype(np.float32)
+    dev = torch.device("cuda")
+    st = torch.as_tensor(states, dtype=torch.float64, device=dev)
+    ac = torch.as_tensor(actions, dtype=torch.float64, device=dev)
+    rtl = torch.full((NT, 1), T, dtype=torch.int64, device=dev)
+    nxt = torch.as_tensor(states[:, 1:].reshape(-1, NF), device=dev)
+    torch.manual_seed(seed)
+    beh = GaussianPolicy(HID, NF, A).to(dev)
+    tgt = GaussianPolicy(HID, NF, A).to(dev)
+    last = GaussianPolicy(HID, NF, A).to(dev)
+    tgt.load_state_dict(beh.state_dict())
+    last.load_state_dict(beh.state_dict())
+    opt_cls = torch.optim.Adam if opt_name == "adam" else torch.optim.RMSprop
+    opt = opt_cls(tgt.parameters(), lr=lr)
+    batch = M.make_particle_batch(st, ac, rtl, nxt, K)
+    return M, (states, actions), beh, tgt, last, opt, batch
+
+
+def _run(monkeypatch, graph, opt_name, lr, kl_threshold, max_off_iters=6):
+    from mepol_amd.algorithms import device_loop
+
+    monkeypatch.setenv("MEPOL_DEVICE_LOOP", "1" if graph else "0")
+    M, raw, beh, tgt, last, opt, (st, ac, rl, _, D, I) = _setup(opt_name, lr)
+    G = float(scipy.special.gamma(NF / 2 + 1))
+    B = float(np.log(K) - scipy.special.digamma(K))
+    trace = []
+    res = M.off_policy_optimization(
+        opt, beh, tgt, last, st, ac, NT, rl, D, I, K, G, B, NF, 0.0, kl_threshold, max_off_iters,
+        True, 2, 4, lr, on_accept=lambda n, e, kl, l: trace.append((n, float(e), float(kl), l)))
+    used = tgt in device_loop._CACHE
+    params = torch.cat([p.detach().reshape(-1) for p in last.parameters()]).cpu().numpy()
+    state = opt.state_dict()["state"]
+    steps = [float(state[i]["step"]) for i in sorted(state)]
+    return dict(H=float(res[0]), n=res[1], bt=res[2], lr=res[3], trace=trace, params=params,
+                steps=steps, used=used, raw=raw, D=D, I=I)
+
+
+@pytest.mark.parametrize("opt_name,lr,kl_threshold", [
+    ("adam", 1e-3, 10.0),     # all steps accepted until max_off_iters
+    ("adam", 5e-2, 1e-3),     # early rejection -> backtracking with halved lr
+    ("rmsprop", 1e-4, 10.0),
+])
+def test_graph_loop_matches_eager(cuda, monkeypatch, opt_name, lr, kl_threshold):
+    g = _run(monkeypatch, True, opt_name, lr, kl_threshold)
+    e = _run(monkeypatch, False, opt_name, lr, kl_threshold)
+    assert g["used"] and not e["used"]
+    assert (g["n"], g["bt"], g["lr"]) == (e["n"], e["bt"], e["lr"])
+    assert g["steps"] == e["steps"]
+    assert len(g["trace"]) == len(e["trace"])
+    for a, b in zip(g["trace"], e["trace"]):
+        assert a[0] == b[0] and a[3] == b[3]
+        np.testing.assert_allclose(a[1:3], b[1:3], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(g["H"], e["H"], rtol=1e-9)
+    np.testing.assert_allclose(g["params"], e["params"], rtol=1e-8, atol=1e-11)
+
+
+def test_graph_loop_matches_oracle(cuda, monkeypatch):
+    """Three accepted Adam steps against the oracle's torch-CPU policy_update/compute_kl."""
+    import oracle.mepol_oracle as O
+
+    g = _run(monkeypatch, True, "adam", 1e-3, 1e9, max_off_iters=3)
+    assert g["used"] and g["n"] == 3
+    states, actions = g["raw"]
+    torch.manual_seed(5)
+    from mepol_amd.policy import GaussianPolicy
+
+    sd = GaussianPolicy(HID, NF, A).state_dict()  # the initial weights _setup drew
+    beh = O.TorchPolicy(HID, NF, A)
+    beh.load_state_dict(sd)
+    tgt = copy.deepcopy(beh)
+    opt = torch.optim.Adam(tgt.parameters(), lr=1e-3)
+    S = torch.as_tensor(states, dtype=torch.float64)
+    Ac = torch.as_tensor(actions, dtype=torch.float64)
+    lengths = torch.full((NT, 1), T, dtype=torch.int64)
+    D, I = g["D"].cpu(), g["I"].cpu()
+    G = float(scipy.special.gamma(NF / 2 + 1))
+    B = float(np.log(K) - scipy.special.digamma(K))
+    for it in range(3):
+        loss, _ = O.torch_policy_update(opt, beh, tgt, S, Ac, NT, lengths, D, I, K, G, B, NF, 0.0)
+        kl, _ = O.torch_kl(beh, tgt, S, Ac, NT, lengths, I, K, 0.0)
+        np.testing.assert_allclose(g["trace"][it][1], -float(loss.detach()), rtol=1e-9)
+        np.testing.assert_allclose(g["trace"][it][2], float(kl), rtol=1e-7, atol=1e-12)
+    p = torch.cat([q.detach().reshape(-1) for q in tgt.parameters()]).numpy()
+    np.testing.assert_allclose(g["params"], p, rtol=1e-7, atol=1e-10)
