@@ -119,6 +119,7 @@ class DeviceIteration:
         self.scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
         self.vals = torch.zeros(2, **f64)
         self.graph = None
+        self.fork = torch.cuda.Stream(device=dev)
         self._batch_id = None
         self._init_state()
 
@@ -216,9 +217,15 @@ class DeviceIteration:
         # through the policy (the _TwoLayerLogp backward)
         dz2, dWm, dbm, dls, db2 = ops.head_backward(grad.view(-1), self.z2, Wm, ls, self.act,
                                                     self.mu, bz=b2, need_dz=True)
-        dW2 = _weight_grad(dz2, self.h1)
+        # dW2 (split-K GEMM) on a forked stream, concurrent with dh1 -> layer-1 backward: the
+        # memory-bound layer kernel overlaps the MFMA-bound GEMM.
+        cur = torch.cuda.current_stream()
+        self.fork.wait_stream(cur)
+        with torch.cuda.stream(self.fork):
+            dW2 = _weight_grad(dz2, self.h1)
         dh1 = torch.mm(dz2, W2)
         dW1, db1 = ops.layer_backward(dh1, self.h1, self.x)
+        cur.wait_stream(self.fork)
         # optimizer.step() (mepol.py:280)
         grad_of = {id(p): g for p, g in zip(self.named, (dW1, db1, dW2, db2, dWm, dbm, dls))}
         ops.optim_step(self.kind, self.params, [grad_of[id(p)] for p in self.params], self.m,
