@@ -500,10 +500,12 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
         # A caller that replaced policy_update / compute_kl (reference-style patching) gets
         # its functions called, not the deferred built-ins.
         deferred = (fns.policy_update, fns.compute_kl) == _BUILTIN_STEP_FNS
-    loop = None
-    if deferred and fns is sys.modules[__name__]:
-        from . import device_loop
+    from . import device_loop
 
+    loop = None
+    if deferred and hasattr(fns, "make_device_loop"):
+        loop = fns.make_device_loop(optimizer, behavioral_policy, target_policy)
+    elif deferred and fns is sys.modules[__name__]:
         batch = P.lookup(states, actions, real_traj_lengths, distances, indices)
         if device_loop.supported(batch, behavioral_policy, target_policy, optimizer):
             loop = device_loop.get(target_policy, optimizer, batch, k, G, B, ns, eps)

@@ -21,9 +21,13 @@ so every rank holds the same H, KL and parameters and takes the same accept/back
 The kernels come from `ops` (the HIP library).  Tests may inject another object with the same
 functions to check this module's collective algebra on CPU with the gloo backend.
 """
+import weakref
+
 import torch
 
 from . import ops as _hip_ops
+from .algorithms.device_loop import DeviceIteration
+from .policy import _weight_grad
 
 
 class ShardedEpoch:
@@ -198,10 +202,148 @@ class ShardedEpoch:
             def compute_entropy(b, t, *a):
                 return self.compute_entropy(b, t, k, G, B, ns, eps)
 
+            @staticmethod
+            def make_device_loop(opt, b, t):
+                return self.device_loop(opt, b, t, G, B, ns, eps)
+
         return off_policy_optimization(optimizer, beh, tgt, last_valid, None, None, self.nt, None,
                                        None, None, k, G, B, ns, eps, kl_threshold, max_off_iters,
                                        use_backtracking, backtrack_coeff, max_backtrack_try,
                                        original_lr, on_accept, fns=_Fns)
+
+
+    # -- graph-replayed iteration (the sharded form of algorithms/device_loop.py) --------------
+    def device_loop(self, optimizer, beh, tgt, G, B, ns, eps):
+        """A ShardedIteration ready for this epoch, or None (eager path).  Every rank takes the
+        same decision: support is a function of identical arguments, and a failed graph capture
+        on any rank turns the graph path off on all of them (all-reduce MIN of a flag)."""
+        from .algorithms import device_loop as DL
+
+        view = _LocalView(self)
+        if not DL.supported(view, beh, tgt, optimizer) or _GRAPH_STATE.get("disabled"):
+            return None
+        if self.dist.get_backend(self.group) != "nccl":  # only RCCL collectives can be captured
+            return None
+        it = _SHARDED_CACHE.get(tgt)
+        if it is None or not it.matches_epoch(tgt, optimizer, self, G, B, ns, eps):
+            _SHARDED_CACHE.pop(tgt, None)
+            it = ShardedIteration(tgt, optimizer, self, G, B, ns, eps)
+            _SHARDED_CACHE[tgt] = it
+        it.attach(self, self.behavioral_logp(beh))
+        if it.graph is None and not it.try_capture():
+            _GRAPH_STATE["disabled"] = True
+            _SHARDED_CACHE.pop(tgt, None)
+            return None
+        it.refresh()
+        return it
+
+
+class _LocalView:
+    """The rank's shard seen through the batch interface DeviceIteration reads."""
+
+    def __init__(self, ep):
+        self.device = ep.dev
+        self.N = ep.n_local
+        self.num_traj = ep.nt
+        self.T = ep.T
+        self.kp1 = ep.D.shape[1]
+        self.states_flat = ep.states_flat
+        self.actions_flat = ep.actions_flat
+        self.D = ep.D
+        self.idx32T = ep.idx32T
+        self.offsets = ep.offsets
+        self.dense = True
+        self._csr = ep.csr
+
+    def csr(self, k):
+        return self._csr
+
+
+_SHARDED_CACHE = weakref.WeakKeyDictionary()  # target policy -> ShardedIteration
+_GRAPH_STATE = {}
+
+
+class ShardedIteration(DeviceIteration):
+    """policy_update + compute_kl of a ShardedEpoch as one graph, with the RCCL all-gathers
+    and the gradient all-reduce of the eager path (same algebra, same order) captured."""
+
+    def __init__(self, tgt, optimizer, ep, G, B, ns, eps):
+        super().__init__(tgt, optimizer, _LocalView(ep), ep.k, G, B, ns, eps)
+        self.dist, self.group, self.world = ep.dist, ep.group, ep.world
+        self.N_global = ep.N
+        self.ep = ep
+
+    def matches_epoch(self, tgt, optimizer, ep, G, B, ns, eps):
+        return (self.matches(tgt, optimizer, _LocalView(ep), ep.k, G, B, ns, eps)
+                and ep.N == self.N_global and ep.world == self.world
+                and ep.dist is self.dist and ep.group is self.group)
+
+    def attach(self, ep, logp_b):
+        self.ep = ep
+        self.load(_LocalView(ep), logp_b)
+
+    def _weights(self, lt):
+        ep, ops = self.ep, self.ep.ops
+        u, ts, _, _ = ops.iw_forward(lt, self.logp_b, self.offsets, self.N, normalize=False)
+        U = ep._sum(ts.sum().reshape(1)).reshape(())
+        w_local = ops.iw_normalize(u, U)
+        return w_local, ep._gather(w_local).reshape(self.N_global)
+
+    @torch.no_grad()
+    def _body(self):
+        ep, ops = self.ep, self.ep.ops
+        W1, b1, W2, b2, Wm, bm, ls = self.named
+        nt, T, k = self.nt, self.T, self.k
+        lt = self.logp.view(nt, T)
+        # H at theta_t (ShardedEpoch.weights / entropy_sums)
+        w_local, w_global = self._weights(lt)
+        out4, _, g = ops.entropy_forward(w_global, self.idx32T, self.D, k, self.ns, self.G,
+                                         self.B, self.eps, n_w=self.N_global)
+        sums_h = ep._sum(out4[2:4].contiguous())
+        # dH/dlogp (_ShardedEntropy.backward)
+        g_global = ep._gather(g).reshape(self.N_global)
+        gamma, partials, nparts = ops.entropy_gamma(g_global, w_local, self.csr_off,
+                                                    self.csr_rows)
+        S = ep._sum(partials[:nparts].sum().reshape(1)).reshape(())
+        grad = ops.entropy_reverse_scan(gamma, w_local, partials, nparts, self.offsets, nt, T,
+                                        self.neg_one, S_ext=S)
+        dz2, dWm, dbm, dls, db2 = ops.head_backward(grad.view(-1), self.z2, Wm, ls, self.act,
+                                                    self.mu, bz=b2, need_dz=True)
+        dW2 = _weight_grad(dz2, self.h1)
+        dh1 = torch.mm(dz2, W2)
+        dW1, db1 = ops.layer_backward(dh1, self.h1, self.x)
+        grad_of = {id(p): t for p, t in zip(self.named, (dW1, db1, dW2, db2, dWm, dbm, dls))}
+        flat = torch.cat([grad_of[id(p)].reshape(-1) for p in self.params])
+        self.dist.all_reduce(flat, group=self.group)  # ShardedEpoch.allreduce_grads
+        grads, o = [], 0
+        for p in self.params:
+            grads.append(flat[o:o + p.numel()].view_as(p))
+            o += p.numel()
+        ops.optim_step(self.kind, self.params, grads, self.m, self.v, self.scal)
+        # KL at theta_t+1 (ShardedEpoch.compute_kl)
+        self.forward()
+        _, w2 = self._weights(lt)
+        out4k, _, _ = ops.entropy_forward(w2, self.idx32T, self.D, k, 1.0, 1.0, 0.0,
+                                          self.eps, n_w=self.N_global)
+        sums_k = ep._sum(out4k[2:4].contiguous())
+        H = -sums_h[0] + self.B
+        KL = sums_k[1] / self.N_global
+        torch.stack((H, KL), out=self.vals)
+
+    def try_capture(self):
+        ok = 1
+        try:
+            self._capture()
+        except Exception:  # capture unsupported here: every rank falls back together
+            self.graph = None
+            ok = 0
+            torch.cuda.synchronize()
+        flag = torch.tensor([ok], dtype=torch.int32, device=self.device)
+        self.dist.all_reduce(flag, op=self.dist.ReduceOp.MIN, group=self.group)
+        if int(flag.item()) == 0:
+            self.graph = None
+            return False
+        return True
 
 
 class _ShardedEntropy(torch.autograd.Function):
