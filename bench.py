@@ -59,8 +59,16 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
-    if world > 1:
+    # MEPOL_BENCH_SHARDED=1 runs the multi-rank code path (ShardedEpoch + captured RCCL
+    # collectives) at world size 1: a one-GPU rehearsal of what --gpus N runs per rank.
+    sharded = world > 1 or os.environ.get("MEPOL_BENCH_SHARDED") == "1"
+    if sharded:
         import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29561")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
 
         backend = os.environ.get("MEPOL_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm
         if backend == "nccl":
@@ -101,7 +109,7 @@ def main():
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         last_valid.load_state_dict(behavioral.state_dict())
-        if world == 1:
+        if not sharded:
             e0.record()
             st_, ac_, rl_, _, D, I = M.make_particle_batch(st, ac, rtl, nxt, k)
             e1.record()
@@ -153,6 +161,11 @@ def main():
             dist.destroy_process_group()
         return
 
+    from mepol_amd import parallel
+    from mepol_amd.algorithms import device_loop
+
+    it = (parallel._SHARDED_CACHE if sharded else device_loop._CACHE).get(target)
+    iteration_path = "hip-graph replay" if it is not None and it.graph is not None else "eager"
     nq = N // world
     F = 3.0 * d * nq * N                      # algorithmic flops
     B_scan = 4.0 * d * nq * N                 # algorithmic scan bytes
@@ -160,7 +173,7 @@ def main():
     knn_gbps = B_scan / (knn_ms * 1e-3) / 1e9
     traffic = None
     pmc_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "knn_pmc.json")
-    if os.path.exists(pmc_path):
+    if os.path.exists(pmc_path) and world == 1:  # counters were taken on the 1-GPU k-NN call
         try:
             traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
         except Exception:
@@ -182,7 +195,8 @@ def main():
                    "particles": N, "num_traj": CFG["num_traj"], "traj_len": CFG["traj_len"],
                    "d": d, "k": k, "policy": f"{nf}->{CFG['hidden']}->{a} f64",
                    "off_policy_iters": float(np.mean(iters_done)), "parallelism": f"dp{world}",
-                   "knn_precision": "fp32 MFMA selection + f64 exact refine (bit-exact output)"},
+                   "knn_precision": "fp32 MFMA selection + f64 exact refine (bit-exact output)",
+                   "off_policy_iteration": iteration_path},
         "particles_per_s": round(N / epoch_s, 1),
         "knn_ms": round(knn_ms, 3),
         "knn_scan_GBps": round(knn_gbps, 1),
