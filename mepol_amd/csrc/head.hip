@@ -24,17 +24,18 @@ constexpr int kMaxCols = 8;   // columns per lane: hidden <= 512
 constexpr double kLog2Pi = 1.8378770664093453;
 constexpr double kStdEps = 1e-7;
 
-// Reduce-scatter of AP per-lane partial sums across the wave: log2(AP) halving exchanges, then
-// a butterfly over the remaining lanes.  Afterwards lane l holds the full sum for
-// a = owner(l) (bit-reversed lane bits 5..), every lane of a group of 64/AP holds the same value.
-template <int AP>
-__device__ __forceinline__ double reduce_scatter(double (&v)[AP], int l, int& a_out) {
+// Reduce-scatter of AP per-lane values over groups of G lanes (G a power of two <= 64, lanes
+// of a group consecutive): halving exchanges, then a butterfly over the remaining lanes.  Lane
+// l ends with the group's sum for component a_out; lanes of a group agreeing on the bits
+// log2(G)-1 .. log2(G)-log2(AP) hold the same component.
+template <int AP, int G>
+__device__ __forceinline__ double reduce_scatter_g(double (&v)[AP], int l, int& a_out) {
   double cur[AP];
 #pragma unroll
   for (int a = 0; a < AP; ++a) cur[a] = v[a];
   int a_idx = 0;
   int len = AP;
-  int bit = 32;
+  int bit = G / 2;
 #pragma unroll
   for (int step = AP; step > 1; step >>= 1) {
     const bool upper = (l & bit) != 0;
@@ -57,89 +58,94 @@ __device__ __forceinline__ double reduce_scatter(double (&v)[AP], int l, int& a_
   return x;
 }
 
-// One wave per row, lane l owns columns c = l + 64 j (j < NC); the lane's slice of Wm lives in
-// VGPRs (NC x AP doubles), rows are software-pipelined (next row's z loads issued before the
-// current row's math), so the kernel streams z at HBM rate with no LDS traffic.
-template <int AP, int NC>
-__global__ __launch_bounds__(256) void head_fwd_kernel(
+// Forward with 16 lanes per row and 4 rows per wave: lane (r = l>>4, q = l&15) owns columns
+// c = q + 16 j (j < NCL) of row 4 i + r.  Each lane runs NCL x AP fma into AP accumulators; the
+// cross-lane reduction is over 16 lanes (4 exchange steps for all AP components) and is shared
+// by 4 rows, so the per-row VALU work is ~H*AP/16 fma + a few exchanges (the 64-lanes-per-row
+// form spent most of its time in the 64-lane reduction and its selects).  Wm, bz and the
+// per-component constants live in LDS; loads of z are 4 rows x 128 B segments, next group
+// prefetched.
+template <int AP, int NCL>
+__global__ __launch_bounds__(256) void head_fwd16_kernel(
     const double* __restrict__ z, int64_t N, int H, const double* __restrict__ bz,
-    const double* __restrict__ Wm,
-    const double* __restrict__ bm, const double* __restrict__ log_std,
-    const double* __restrict__ act, int A, double* __restrict__ mu_out,
-    double* __restrict__ logp_out) {
-  __shared__ double sW[NC * 64 * AP];  // [j][a][lane]: lane-contiguous, conflict-free
+    const double* __restrict__ Wm, const double* __restrict__ bm,
+    const double* __restrict__ log_std, const double* __restrict__ act, int A,
+    double* __restrict__ mu_out, double* __restrict__ logp_out) {
+  constexpr int AP2 = AP >= 2 ? AP / 2 : 1;
+  __shared__ double2 sW2[NCL * AP2 * 16];  // [j][a/2][q] pairs (a even, a+1)
+  __shared__ double sB[NCL * 16];          // [j][q] folded bias of z
+  __shared__ double sK[3][AP];             // bm, log 2pi + 2 log_std, 1/sigma^2
   const int l = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int e = threadIdx.x; e < NC * 64 * AP; e += blockDim.x) {
-    const int ll = e & 63, a = (e >> 6) % AP, j = (e >> 6) / AP;
-    const int c = ll + 64 * j;
-    sW[e] = (c < H && a < A) ? Wm[a * H + c] : 0.0;
+  const int q = l & 15, r = l >> 4;
+  for (int e = threadIdx.x; e < NCL * AP2 * 16; e += blockDim.x) {
+    const int qq = e & 15, a2 = (e >> 4) % AP2, j = (e >> 4) / AP2;
+    const int c = qq + 16 * j;
+    const int a0 = 2 * a2, a1 = 2 * a2 + 1;
+    double2 w;
+    w.x = (c < H && a0 < A) ? Wm[a0 * H + c] : 0.0;
+    w.y = (AP >= 2 && c < H && a1 < A) ? Wm[a1 * H + c] : 0.0;
+    sW2[e] = w;
   }
-  __syncthreads();
-  double bzr[NC];  // last hidden layer's bias, folded in here (its GEMM runs without bias)
-#pragma unroll
-  for (int j = 0; j < NC; ++j) bzr[j] = (bz && l + 64 * j < H) ? bz[l + 64 * j] : 0.0;
-  double zn[NC];
-  auto load_row = [&](int64_t i) {
-#pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      const int c = l + 64 * j;
-      zn[j] = (i < N && c < H) ? z[i * H + c] : 0.0;
-    }
-  };
-  double bmu[AP], cst[AP], is2[AP];  // wave-uniform constants (scalar registers)
-#pragma unroll
-  for (int a = 0; a < AP; ++a) {
+  for (int e = threadIdx.x; e < NCL * 16; e += blockDim.x) sB[e] = (bz && e < H) ? bz[e] : 0.0;
+  if (threadIdx.x < AP) {
+    const int a = threadIdx.x;
     const double lsa = (a < A) ? log_std[a] : 0.0;
     const double sd = exp(lsa) + kStdEps;
-    bmu[a] = (a < A) ? bm[a] : 0.0;
-    cst[a] = kLog2Pi + 2.0 * lsa;
-    is2[a] = 1.0 / (sd * sd);
+    sK[0][a] = (a < A) ? bm[a] : 0.0;
+    sK[1][a] = kLog2Pi + 2.0 * lsa;
+    sK[2][a] = 1.0 / (sd * sd);
   }
+  __syncthreads();
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t ngroups = (N + 3) / 4;
+  double zn[NCL];
+  auto load_group = [&](int64_t gi) {
+    const int64_t row = gi * 4 + r;
+#pragma unroll
+    for (int j = 0; j < NCL; ++j) {
+      const int c = q + 16 * j;
+      zn[j] = (row < N && c < H) ? z[row * H + c] : 0.0;
+    }
+  };
   const int64_t wave_u = __builtin_amdgcn_readfirstlane((int)wave);
-  load_row(wave_u);
-  for (int64_t i = wave_u; i < N; i += nwaves) {
-    // row-uniform scalar loads first, so waiting on them never drains the z prefetch below
-    double av[AP];
+  load_group(wave_u);
+  for (int64_t gi = wave_u; gi < ngroups; gi += nwaves) {
+    double zc[NCL];
 #pragma unroll
-    for (int a = 0; a < AP; ++a) av[a] = (a < A) ? act[i * A + a] : 0.0;
-    double zc[NC];
-#pragma unroll
-    for (int j = 0; j < NC; ++j) zc[j] = zn[j];
-    load_row(i + nwaves);
+    for (int j = 0; j < NCL; ++j) zc[j] = zn[j];
+    load_group(gi + nwaves);
+    const int64_t row = gi * 4 + r;
     double acc[AP];
 #pragma unroll
     for (int a = 0; a < AP; ++a) acc[a] = 0.0;
-    int lo = l;
-    asm volatile("" : "+v"(lo));  // keep the Wm LDS reads in the loop (no hoist into VGPRs)
+    int qo = q;
+    asm volatile("" : "+v"(qo));  // keep the LDS reads inside the loop
 #pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      const double x = fmax(zc[j] + bzr[j], 0.0);
+    for (int j = 0; j < NCL; ++j) {
+      const double x = fmax(zc[j] + sB[j * 16 + qo], 0.0);
 #pragma unroll
-      for (int a = 0; a < AP; ++a) acc[a] += x * sW[(j * AP + a) * 64 + lo];
+      for (int a2 = 0; a2 < AP2; ++a2) {
+        const double2 w = sW2[(j * AP2 + a2) * 16 + qo];
+        acc[2 * a2] = fma(x, w.x, acc[2 * a2]);
+        if (AP >= 2) acc[2 * a2 + 1] = fma(x, w.y, acc[2 * a2 + 1]);
+      }
     }
     int a;
-    const double v = reduce_scatter<AP>(acc, l, a);
+    const double v = reduce_scatter_g<AP, 16>(acc, l, a);
+    // lanes of a row with equal component: (16 / AP) of them; the lowest one writes
+    const bool writer = (q & ((16 / AP) - 1)) == 0;
     double term = 0.0;
-    const bool writer = (l & ((64 / AP) - 1)) == 0;  // one lane per action component
-    double b_a = 0.0, c_a = 0.0, i_a = 0.0, x_a = 0.0;
-#pragma unroll
-    for (int q = 0; q < AP; ++q)
-      if (a == q) {
-        b_a = bmu[q];
-        c_a = cst[q];
-        i_a = is2[q];
-        x_a = av[q];
-      }
-    if (a < A && writer) {
-      const double m = v + b_a;
-      const double d = x_a - m;
-      mu_out[i * A + a] = m;
-      term = -0.5 * (c_a + d * d * i_a);
+    if (row < N && a < A && writer) {
+      const double m = v + sK[0][a];
+      const double d = act[row * A + a] - m;
+      mu_out[row * A + a] = m;
+      term = -0.5 * (sK[1][a] + d * d * sK[2][a]);
     }
-    const double lp = wave_sum(term);
-    if (l == 0) logp_out[i] = lp;
+    // logp_row = sum over the row's 16 lanes (non-writers hold 0)
+#pragma unroll
+    for (int bit = 8; bit >= 1; bit >>= 1) term += __shfl_xor(term, bit, kWave);
+    if (q == 0 && row < N) logp_out[row] = term;
   }
 }
 
@@ -232,8 +238,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       double dh = 0.0;
 #pragma unroll
       for (int a = 0; a < AP; ++a) {
-        dh += dm[a] * sW[(j * AP + a) * 64 + lo];
-        accW[j][a] += dm[a] * x;
+        dh = fma(dm[a], sW[(j * AP + a) * 64 + lo], dh);
+        accW[j][a] = fma(dm[a], x, accW[j][a]);
       }
       const double dzv = (zb > 0.0) ? dh : 0.0;
       accz[j] += dzv;
@@ -316,10 +322,6 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __re
   }
 }
 
-static int grid_for(int64_t N) {
-  const int64_t waves = (N + 7) / 8;  // >= 8 rows per wave
-  return (int)std::max<int64_t>(1, std::min<int64_t>(1024, (waves + 3) / 4));
-}
 static int grid_bwd(int64_t N) {
   const int64_t waves = (N + 31) / 32;  // >= 32 rows per wave
   return (int)std::max<int64_t>(1, std::min<int64_t>(512, (waves + 3) / 4));
@@ -342,16 +344,19 @@ extern "C" int mepol_head_forward(const double* z, int64_t n, int hidden, const 
   }
   if (n == 0) return 0;
   const int ap = a_dim <= 1 ? 1 : a_dim <= 2 ? 2 : a_dim <= 4 ? 4 : 8;
-  const int nc = (hidden + 63) / 64;
-  dim3 g(grid_for(n));
+  const int ncl16 = (hidden + 15) / 16;
+  const int ncl = ncl16 <= 4 ? 4 : ncl16 <= 8 ? 8 : ncl16 <= 12 ? 12 : ncl16 <= 16 ? 16
+                : ncl16 <= 20 ? 20 : ncl16 <= 24 ? 24 : 32;
+  const int64_t groups = (n + 3) / 4;
+  dim3 g((unsigned)std::max<int64_t>(1, std::min<int64_t>(1024, (groups / 4 + 3) / 4)));
   hipStream_t st = (hipStream_t)stream;
-#define MEPOL_HEAD_FWD(AP_, NC_)                                                                \
-  if (ap == AP_ && nc == NC_)                                                                   \
-    hipLaunchKernelGGL((head_fwd_kernel<AP_, NC_>), g, dim3(256), 0, st, z, n, hidden, bz, Wm,  \
+#define MEPOL_HEAD_FWD(AP_, NC_)                                                                 \
+  if (ap == AP_ && ncl == NC_)                                                                   \
+    hipLaunchKernelGGL((head_fwd16_kernel<AP_, NC_>), g, dim3(256), 0, st, z, n, hidden, bz, Wm, \
                        bm, log_std, act, a_dim, mu_out, logp_out);
-#define MEPOL_HEAD_FWD_A(AP_) \
-  MEPOL_HEAD_FWD(AP_, 1) MEPOL_HEAD_FWD(AP_, 2) MEPOL_HEAD_FWD(AP_, 3) MEPOL_HEAD_FWD(AP_, 4) \
-  MEPOL_HEAD_FWD(AP_, 5) MEPOL_HEAD_FWD(AP_, 6) MEPOL_HEAD_FWD(AP_, 7) MEPOL_HEAD_FWD(AP_, 8)
+#define MEPOL_HEAD_FWD_A(AP_)                                                               \
+  MEPOL_HEAD_FWD(AP_, 4) MEPOL_HEAD_FWD(AP_, 8) MEPOL_HEAD_FWD(AP_, 12) MEPOL_HEAD_FWD(AP_, 16) \
+  MEPOL_HEAD_FWD(AP_, 20) MEPOL_HEAD_FWD(AP_, 24) MEPOL_HEAD_FWD(AP_, 32)
   MEPOL_HEAD_FWD_A(1) MEPOL_HEAD_FWD_A(2) MEPOL_HEAD_FWD_A(4) MEPOL_HEAD_FWD_A(8)
 #undef MEPOL_HEAD_FWD_A
 #undef MEPOL_HEAD_FWD
