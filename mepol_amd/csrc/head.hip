@@ -19,6 +19,10 @@
 namespace mepol {
 namespace head {
 
+#ifndef MEPOL_HEAD_BWD_PF
+#define MEPOL_HEAD_BWD_PF 1  // rows prefetched per wave in head_bwd_kernel
+#endif
+
 constexpr int kMaxA = 8;      // fused path: action_dim <= 8 (MountainCar 1, GridWorld 2, Ant 8)
 constexpr int kMaxCols = 8;   // columns per lane: hidden <= 512
 constexpr double kLog2Pi = 1.8378770664093453;
@@ -100,12 +104,14 @@ __global__ __launch_bounds__(256) void head_fwd16_kernel(
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int64_t ngroups = (N + 3) / 4;
   double zn[NCL];
-  auto load_group = [&](int64_t gi) {
+  const int64_t last = N - 1;
+  auto load_group = [&](int64_t gi) {  // clamped, unconditional loads (see head_bwd_kernel)
     const int64_t row = gi * 4 + r;
+    const double* zr = z + (row < N ? row : last) * H;
 #pragma unroll
     for (int j = 0; j < NCL; ++j) {
       const int c = q + 16 * j;
-      zn[j] = (row < N && c < H) ? z[row * H + c] : 0.0;
+      zn[j] = zr[c < H ? c : H - 1];
     }
   };
   const int64_t wave_u = __builtin_amdgcn_readfirstlane((int)wave);
@@ -194,39 +200,53 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     bzr[j] = (bz && l + 64 * j < H) ? bz[l + 64 * j] : 0.0;
     accz[j] = 0.0;
   }
-  double zn[NC];
-  auto load_row = [&](int64_t i) {
+  // kPF rows in flight per wave: z row (VGPRs) + its row-uniform g / act / mu (SGPRs) are
+  // loaded kPF rows ahead (register ring; slots are compile-time after unrolling).
+  constexpr int kPF = MEPOL_HEAD_BWD_PF;
+  struct Slot {
+    double z[NC];
+    double g, av[AP], mv[AP];
+  };
+  Slot ring[kPF];
+  // Unconditional loads from clamped (in-bounds) addresses: no exec-mask branches around the
+  // loads, so they issue back to back and stay in flight.  Values of clamped columns / rows /
+  // components are never used (zero weights / bias, guarded stores, guarded rows, zeroed a >= A).
+  const int64_t last = N - 1;
+  auto load_slot = [&](Slot& dst, int64_t i) {
+    const int64_t ic = i < N ? i : last;
+    const double* zr = z + ic * H;
 #pragma unroll
     for (int j = 0; j < NC; ++j) {
       const int c = l + 64 * j;
-      zn[j] = (i < N && c < H) ? z[i * H + c] : 0.0;
+      dst.z[j] = zr[c < H ? c : H - 1];
+    }
+    dst.g = gl[ic];
+#pragma unroll
+    for (int a = 0; a < AP; ++a) {
+      const int ac = a < A ? a : A - 1;
+      dst.av[a] = act[ic * A + ac];
+      dst.mv[a] = mu[ic * A + ac];
     }
   };
-  const int64_t wave_u = __builtin_amdgcn_readfirstlane((int)wave);
-  load_row(wave_u);
-  for (int64_t i = wave_u; i < N; i += nwaves) {
-    // row-uniform scalar loads first (they do not count against the z prefetch's vmcnt)
-    const double g = gl[i];
-    double av[AP], mv[AP];
-#pragma unroll
-    for (int a = 0; a < AP; ++a) {
-      av[a] = (a < A) ? act[i * A + a] : 0.0;
-      mv[a] = (a < A) ? mu[i * A + a] : 0.0;
-    }
+  auto row_step = [&](int64_t i, Slot& slot) {
     double zc[NC];
 #pragma unroll
-    for (int j = 0; j < NC; ++j) zc[j] = zn[j];
-    load_row(i + nwaves);
-    double dm[AP];  // every lane computes all dmu_a from row-uniform loads
+    for (int j = 0; j < NC; ++j) zc[j] = slot.z[j];
+    const double g = slot.g;
+    double dm[AP];  // every lane computes all dmu_a from row-uniform values
+    double db_l = 0.0, dls_l = 0.0;
 #pragma unroll
     for (int a = 0; a < AP; ++a) {
-      const double d = av[a] - mv[a];
+      const double d = (a < A) ? slot.av[a] - slot.mv[a] : 0.0;
       dm[a] = g * d * sInv[a];
       if (a == l) {
-        accb += dm[a];
-        accls += g * (-1.0 + d * d * es3);
+        db_l = dm[a];
+        dls_l = g * (-1.0 + d * d * es3);
       }
     }
+    accb += db_l;
+    accls += dls_l;
+    load_slot(slot, i + kPF * nwaves);
     double* dzr = dz ? dz + i * H : nullptr;
     int lo = l;
     asm volatile("" : "+v"(lo));  // keep the Wm LDS reads in the loop (no hoist into VGPRs)
@@ -245,6 +265,14 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       accz[j] += dzv;
       if (dzr && c < H) dzr[c] = dzv;
     }
+  };
+  const int64_t wave_u = __builtin_amdgcn_readfirstlane((int)wave);
+#pragma unroll
+  for (int p = 0; p < kPF; ++p) load_slot(ring[p], wave_u + p * nwaves);
+  for (int64_t i = wave_u; i < N; i += kPF * nwaves) {
+#pragma unroll
+    for (int p = 0; p < kPF; ++p)
+      if (i + p * nwaves < N) row_step(i + p * nwaves, ring[p]);
   }
   // block reduction in a fixed order (waves 0..3), then one record per block
   if (l < AP) {

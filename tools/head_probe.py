@@ -41,6 +41,7 @@ mu, lp = ops.head_forward(z, Wm, bm, ls, act, bz=bz)
 res = {
     "head_fwd": t(lambda: ops.head_forward(z, Wm, bm, ls, act, bz=bz, mu_out=mu, logp_out=lp)),
     "head_bwd": t(lambda: ops.head_backward(gl, z, Wm, ls, act, mu, bz=bz)),
+    "head_bwd_nodz": t(lambda: ops.head_backward(gl, z, Wm, ls, act, mu, bz=bz, need_dz=False)),
     "layer_fwd": t(lambda: ops.layer_forward(x, W1, b1, out=h1)),
     "layer_bwd": t(lambda: ops.layer_backward(dh, h1, x)),
 }
