@@ -25,12 +25,14 @@
 #include <algorithm>
 #include <cfloat>
 #include <climits>
+#include <cstdlib>
 
 namespace mepol {
 namespace knn {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
 
 constexpr float kPadNorm = 1e30f;  // |c|^2 of padding candidates: never selected
 constexpr int kBufCap = 24;        // per-lane LDS insertion buffer (entries)
@@ -255,6 +257,254 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ a
 }
 
 // ---------------------------------------------------------------------------------------
+// 2b. select on split-f16 MFMA (default): the same |c|^2 - 2 q.c, with every operand split
+//     into two f16 halves, a = a_hi + a_lo (|a - a_hi - a_lo| <= 2^-22 |a|), and the three
+//     products hi*hi + hi*lo + lo*hi accumulated in f32 by v_mfma_f32_32x32x16_f16 (exact
+//     products, f32 sums): ~f32-class accuracy at 3 MFMAs of 16x the f32 rate.  Coordinates
+//     are scaled by a power of two sigma (max norm -> (64, 128]) so |c|^2 fits f16; outputs
+//     are unscaled exactly.  refine's certification uses this path's error bound.
+// ---------------------------------------------------------------------------------------
+// max |x| over candidates (scal[0]) and over queries (scal[2]), non-negative float bit order.
+__global__ __launch_bounds__(256) void norms_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                    unsigned* __restrict__ out_bits) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float nrm = 0.f;
+  if (i < n) {
+    const float* x = X + i * d;
+    float s2 = 0.f;
+    for (int f = 0; f < d; ++f) s2 = fmaf(x[f], x[f], s2);
+    nrm = sqrtf(s2);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) nrm = fmaxf(nrm, __shfl_xor(nrm, m, kWave));
+  if ((threadIdx.x & 63) == 0) atomicMax(out_bits, __float_as_uint(nrm));
+}
+
+// sigma = 2^e with sigma * max(cmax, qmax) in (64, 128] (1 when the data is all zero).
+__device__ __forceinline__ float knn_scale(const unsigned* __restrict__ scal) {
+  const float m = fmaxf(__uint_as_float(scal[0]), __uint_as_float(scal[2]));
+  // slack for the f32 rounding of sqrt in norms_kernel: 127.9 instead of 128
+  if (!(m > 0.f) || !(m < 3e38f)) return 1.f;
+  int e;
+  (void)frexpf(127.9f / m, &e);
+  e = max(-100, min(100, e - 1));
+  return ldexpf(1.f, e);
+}
+
+__device__ __forceinline__ void split_f16(float v, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)v;
+  lo = (_Float16)(v - (float)hi);  // v - hi is exact in f32
+}
+
+constexpr float kPadNorm16 = 60000.f;  // scaled |c|^2 of padding candidates (> any real D')
+
+// apack16[((t*64 + l)*KS16 + s)*16 + {0..7 hi, 8..15 lo}] = A[i = l&31][k = 16 s + 8 (l>>5) + j]
+// of candidate tile t: f<d: -2 sigma x_cf ; f==d: |sigma c|^2 ; else 0.
+__global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X, int64_t n, int d,
+                                                     int KS16, int64_t nct,
+                                                     _Float16* __restrict__ apack,
+                                                     const unsigned* __restrict__ scal) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= nct * 64) return;
+  const float sg = knn_scale(scal);
+  const int64_t t = gid >> 6;
+  const int l = (int)(gid & 63);
+  const int h = l >> 5;
+  const int64_t c = t * 32 + (l & 31);
+  const bool valid = c < n;
+  float cn = 0.f;
+  if (valid) {
+    const float* xc = X + c * d;
+    for (int f = 0; f < d; ++f) {
+      const float y = sg * xc[f];
+      cn = fmaf(y, y, cn);
+    }
+  }
+  _Float16* dst = apack + gid * KS16 * 16;
+  for (int s = 0; s < KS16; ++s) {
+    f16x8 hv, lv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * s + 8 * h + j;
+      float v;
+      if (valid)
+        v = (f < d) ? -2.f * sg * X[c * d + f] : ((f == d) ? cn : 0.f);
+      else
+        v = (f == d) ? kPadNorm16 : 0.f;
+      _Float16 a, b;
+      split_f16(v, a, b);
+      hv[j] = a;
+      lv[j] = b;
+    }
+    *reinterpret_cast<f16x8*>(dst + s * 16) = hv;
+    *reinterpret_cast<f16x8*>(dst + s * 16 + 8) = lv;
+  }
+}
+
+template <int KS16, int LIST>
+__global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restrict__ apack,
+                                                       const float* __restrict__ query,
+                                                       int64_t nq, int d, int64_t nct, int split,
+                                                       int64_t tiles_per_split,
+                                                       const unsigned* __restrict__ scal,
+                                                       float* __restrict__ out_v,
+                                                       int* __restrict__ out_i) {
+  __shared__ float sbuf_v[4][kBufCap][64];
+  __shared__ int sbuf_i[4][kBufCap][64];
+  const int w = threadIdx.x >> 6;
+  const int l = threadIdx.x & 63;
+  const int64_t qt = (int64_t)blockIdx.x * 4 + w;
+  const int sp = blockIdx.y;
+  if (qt * 32 >= nq) return;  // wave-uniform
+  const int h = l >> 5;
+  const int64_t q = qt * 32 + (l & 31);
+  const bool qvalid = q < nq;
+  const float sg = knn_scale(scal);
+  const float inv_s2 = 1.f / (sg * sg);  // exact: sigma is a power of two
+
+  // B operand (queries): B[k = 16 s + 8h + j][col = l&31] = sigma q_f (f<d), 1 (f==d), 0.
+  f16x8 bhi[KS16], blo[KS16];
+#pragma unroll
+  for (int s = 0; s < KS16; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * s + 8 * h + j;
+      const float v = qvalid ? ((f < d) ? sg * query[q * d + f] : ((f == d) ? 1.f : 0.f)) : 0.f;
+      _Float16 a, b;
+      split_f16(v, a, b);
+      bhi[s][j] = a;
+      blo[s][j] = b;
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int s = 0; s < KS16; ++s) {
+    f32x4 x = __builtin_bit_cast(f32x4, bhi[s]);
+    f32x4 y = __builtin_bit_cast(f32x4, blo[s]);
+    asm volatile("" : "+v"(x), "+v"(y));
+    bhi[s] = __builtin_bit_cast(f16x8, x);
+    blo[s] = __builtin_bit_cast(f16x8, y);
+  }
+
+  float ld[LIST];
+  int li[LIST];
+#pragma unroll
+  for (int j = 0; j < LIST; ++j) {
+    ld[j] = INFINITY;
+    li[j] = -1;
+  }
+  float thr = INFINITY;
+  int cnt = 0;
+
+  const int64_t t0 = (int64_t)sp * tiles_per_split;
+  const int64_t t1 = min(nct, t0 + tiles_per_split);
+
+  // Three fragment buffers: tile t's MFMAs run while tile t-1's threshold work executes and
+  // tile t+1's loads are in flight; a buffer is refilled (tile t+2) only after the chain that
+  // read it has completed (its results were consumed).  Loads are inline asm with hand-counted
+  // waits (NV per tile; no other vector-memory op in the loop).
+  constexpr int NV = 2 * KS16;  // dwordx4 per lane per tile: hi and lo halves of each k-step
+  const f32x4* abase = reinterpret_cast<const f32x4*>(apack) + (int64_t)l * NV;
+  f32x4 Bf[3][NV];
+  auto load = [&](f32x4 (&A)[NV], int64_t t) {
+    const f32x4* p = abase + t * 64 * NV;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      f32x4 x;
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(p + v) : "memory");
+      A[v] = x;
+    }
+  };
+  auto landed = [&](f32x4 (&A)[NV]) {  // all but the NV youngest loads (next tile) have landed
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV) : "memory");
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      f32x4 x = A[v];
+      asm volatile("" : "+v"(x));
+      A[v] = x;
+    }
+  };
+  auto chain = [&](const f32x4 (&A)[NV]) -> f32x16 {
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < KS16; ++s) {
+      const f16x8 ah = __builtin_bit_cast(f16x8, A[2 * s]);
+      const f16x8 al = __builtin_bit_cast(f16x8, A[2 * s + 1]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bhi[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, blo[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bhi[s], acc, 0, 0, 0);
+    }
+    return acc;
+  };
+  auto process = [&](f32x16 acc, int64_t t) {
+    float m = fminf(fminf(fminf(acc[0], acc[1]), fminf(acc[2], acc[3])),
+                    fminf(fminf(acc[4], acc[5]), fminf(acc[6], acc[7])));
+    m = fminf(m, fminf(fminf(fminf(acc[8], acc[9]), fminf(acc[10], acc[11])),
+                       fminf(fminf(acc[12], acc[13]), fminf(acc[14], acc[15]))));
+    if (__ballot(m < thr)) {
+      const int base = (int)(t * 32);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (acc[r] < thr) {
+          sbuf_v[w][cnt][l] = acc[r];
+          sbuf_i[w][cnt][l] = base + acc_row(r, l);
+          ++cnt;
+        }
+      }
+      if (__ballot(cnt > kBufCap - 16)) flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l);
+    }
+  };
+  if (t0 < t1) {
+    const int64_t tl = t1 - 1;
+    load(Bf[0], t0);
+    load(Bf[1], min(t0 + 1, tl));
+    landed(Bf[0]);
+    f32x16 accP = chain(Bf[0]);
+    load(Bf[2], min(t0 + 2, tl));
+    int64_t t = t0 + 1;
+    // steady state, unrolled by 3 so buffer indices are compile-time: at step t the tile is in
+    // Bf[(t - t0) % 3], the chain of t-1 read Bf[(t - t0 - 1) % 3] (refilled with t+2).
+#define MEPOL_SEL16_STEP(CUR, PREV)         \
+  {                                         \
+    landed(Bf[CUR]);                        \
+    const f32x16 accN = chain(Bf[CUR]);     \
+    process(accP, t - 1);                   \
+    load(Bf[PREV], min(t + 2, tl));         \
+    accP = accN;                            \
+    ++t;                                    \
+  }
+#pragma nounroll
+    while (t + 2 < t1) {
+      MEPOL_SEL16_STEP(1, 0)
+      MEPOL_SEL16_STEP(2, 1)
+      MEPOL_SEL16_STEP(0, 2)
+    }
+    // remainder (0..2 tiles), same buffer rotation
+    if (t < t1) MEPOL_SEL16_STEP(1, 0)
+    if (t < t1) MEPOL_SEL16_STEP(2, 1)
+#undef MEPOL_SEL16_STEP
+    // Retire every outstanding fragment load and keep all three buffers live up to here: the
+    // last prefetches are never consumed, and an asm load whose output the compiler thinks is
+    // dead may be given registers that a later instruction reuses while the data is in flight.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[b][v]));
+    process(accP, t - 1);
+  }
+  flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l);
+
+  if (qvalid) {
+    const int64_t o = ((q * split + sp) * 2 + h) * LIST;
+#pragma unroll
+    for (int j = 0; j < LIST; ++j) {
+      out_v[o + j] = ld[j] * inv_s2;
+      out_i[o + j] = li[j];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // 3. refine + certify
 // ---------------------------------------------------------------------------------------
 __device__ __forceinline__ bool lex_less(double a, int ai, double b, int bi) {
@@ -293,8 +543,9 @@ template <int LIST, int MAXP>
 __global__ __launch_bounds__(256) void refine_kernel(
     const float* __restrict__ cand, int64_t nc, const float* __restrict__ query, int64_t nq, int d,
     int kp1, int split, const float* __restrict__ lists_v, const int* __restrict__ lists_i,
-    const unsigned* __restrict__ cmax_bits, double* __restrict__ Dout, int64_t* __restrict__ I64,
-    int32_t* __restrict__ I32, int* __restrict__ flag_count, int* __restrict__ flag_list) {
+    const unsigned* __restrict__ cmax_bits, int e_terms, double* __restrict__ Dout,
+    int64_t* __restrict__ I64, int32_t* __restrict__ I32, int* __restrict__ flag_count,
+    int* __restrict__ flag_list) {
   __shared__ int sel[4][64];
   const int w = threadIdx.x >> 6;
   const int l = threadIdx.x & 63;
@@ -391,8 +642,10 @@ __global__ __launch_bounds__(256) void refine_kernel(
   double qn2 = 0.0;
   for (int f = 0; f < d; ++f) qn2 += (double)xq[f] * (double)xq[f];
   const double cmax = (double)__uint_as_float(*cmax_bits);
-  const double E = 4.0 * (double)(d + 1) * 5.9604644775390625e-08 * (cmax * cmax + cmax * sqrt(qn2)) +
-                   1e-300;
+  // e_terms * 2^-24 * (C^2 + 2 C |q|) bounds the selection's error (f32 path: 4 (d + 1);
+  // split-f16 path: 2 (3 K + 16 + d), see make_plan), C = max candidate norm.
+  const double E = (double)e_terms * 5.9604644775390625e-08 *
+                       (cmax * cmax + 2.0 * cmax * sqrt(qn2)) + 1e-300;
   const double ek = __shfl(dd, kp1 - 1, kWave);
   const int eki = __shfl(di, kp1 - 1, kWave);
   bool ok = (eki != INT_MAX);
@@ -509,6 +762,9 @@ __global__ void fill_identity_kernel(int* s, int64_t n) {
 // ---------------------------------------------------------------------------------------
 struct Plan {
   int d, kp1, KS, KSP, LIST, split, maxp;
+  int mode;       // 0: f32 MFMA selection, 1: split-f16 MFMA selection (default, d + 1 <= 64)
+  int KS16;       // k-steps of 16 (mode 1)
+  int e_terms;    // selection error bound multiplier (refine certification)
   int64_t nc, nq, nct, nqt, tiles_per_split;
   size_t off_apack, off_scalars, off_lv, off_li, off_flag, total;
 };
@@ -550,6 +806,19 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   }
   P->d = d;
   P->kp1 = kp1;
+  {
+    const char* prec = getenv("MEPOL_KNN_PRECISION");
+    const bool want_f32 = prec && (prec[0] == 'f' && prec[1] == '3' && prec[2] == '2');
+    P->KS16 = (d + 1 + 15) / 16;
+    // split-f16 instantiations that stay below the 256-VGPR cap (at the cap the fragment
+    // buffers of the asm-load pipeline are no longer safe from register copies)
+    const bool fits = P->KS16 == 1 || (P->KS16 == 2 && LIST <= 40) ||
+                      (P->KS16 == 3 && LIST <= 40);
+    P->mode = (!want_f32 && fits) ? 1 : 0;
+    // f32: d + 1 fma-chain roundings, x4 margin.  split-f16: 3 K products per output summed in
+    // f32 (<= 3K roundings), operand splitting 3 * 2^-22 = 12 * 2^-24, |c|^2 in f32 (d), x2.
+    P->e_terms = P->mode ? 2 * (3 * 16 * P->KS16 + 16 + d) : 4 * (d + 1);
+  }
   P->KS = KS;
   P->KSP = (KS + 3) / 4 * 4;
   P->LIST = LIST;
@@ -570,7 +839,9 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   P->maxp = (2 * split * LIST + 63) / 64;
   size_t off = 0;
   P->off_apack = off;
-  off = align_up(off + (size_t)P->nct * 64 * P->KSP * sizeof(float), 256);
+  off = align_up(off + std::max((size_t)P->nct * 64 * P->KSP * sizeof(float),
+                                (size_t)P->nct * 64 * P->KS16 * 16 * sizeof(_Float16)),
+                 256);
   P->off_scalars = off;
   off = align_up(off + 16, 256);
   const size_t nl = (size_t)std::max<int64_t>(nq, 1) * 2 * split * LIST;
@@ -608,6 +879,21 @@ static void launch_select_ks(const Plan& P, dim3 g, const float* ap, const float
   }
 }
 
+template <int KS16>
+static void launch_select16_ks(const Plan& P, dim3 g, const _Float16* ap, const float* query,
+                               const unsigned* scal, float* lv, int* li, hipStream_t st) {
+#define MEPOL_SEL16(L)                                                                          \
+  hipLaunchKernelGGL((select16_kernel<KS16, L>), g, dim3(256), 0, st, ap, query, P.nq, P.d, P.nct, \
+                     P.split, P.tiles_per_split, scal, lv, li)
+  switch (P.LIST) {
+    case 8: MEPOL_SEL16(8); break;
+    case 16: MEPOL_SEL16(16); break;
+    case 40: MEPOL_SEL16(40); break;
+    default: MEPOL_SEL16(64); break;
+  }
+#undef MEPOL_SEL16
+}
+
 template <int LIST>
 static void launch_refine_list(const Plan& P, const float* cand, const float* query,
                                const float* lv, const int* li, const unsigned* cmax, double* D,
@@ -616,19 +902,19 @@ static void launch_refine_list(const Plan& P, const float* cand, const float* qu
   // MAXP = ceil(2 * split * LIST / 64) for split <= kMaxSplit
   if (P.maxp <= 2)
     hipLaunchKernelGGL((refine_kernel<LIST, 2>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.split, lv, li, cmax, D, I64, I32, fc, fl);
+                       P.kp1, P.split, lv, li, cmax, P.e_terms, D, I64, I32, fc, fl);
   else if (P.maxp <= 4)
     hipLaunchKernelGGL((refine_kernel<LIST, 4>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.split, lv, li, cmax, D, I64, I32, fc, fl);
+                       P.kp1, P.split, lv, li, cmax, P.e_terms, D, I64, I32, fc, fl);
   else if (P.maxp <= 8)
     hipLaunchKernelGGL((refine_kernel<LIST, 8>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.split, lv, li, cmax, D, I64, I32, fc, fl);
+                       P.kp1, P.split, lv, li, cmax, P.e_terms, D, I64, I32, fc, fl);
   else if (P.maxp <= 16)
     hipLaunchKernelGGL((refine_kernel<LIST, 16>), g, dim3(256), 0, st, cand, P.nc, query, P.nq,
-                       P.d, P.kp1, P.split, lv, li, cmax, D, I64, I32, fc, fl);
+                       P.d, P.kp1, P.split, lv, li, cmax, P.e_terms, D, I64, I32, fc, fl);
   else
     hipLaunchKernelGGL((refine_kernel<LIST, 32>), g, dim3(256), 0, st, cand, P.nc, query, P.nq,
-                       P.d, P.kp1, P.split, lv, li, cmax, D, I64, I32, fc, fl);
+                       P.d, P.kp1, P.split, lv, li, cmax, P.e_terms, D, I64, I32, fc, fl);
 }
 
 template <int LIST>
@@ -692,13 +978,30 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
 
   MEPOL_HIP(hipMemsetAsync(ws + P.off_scalars, 0, 16, st));
   if (n_fallback_out) MEPOL_HIP(hipMemsetAsync(n_fallback_out, 0, sizeof(int32_t), st));
-  {
+  if (P.mode == 1) {
+    // scal[0] = max candidate norm (refine's C), scal[2] = max query norm (scale only)
+    hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nc + 255) / 256)), dim3(256), 0, st, cand,
+                       P.nc, P.d, cmax);
+    hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nq + 255) / 256)), dim3(256), 0, st, query,
+                       P.nq, P.d, cmax + 2);
+    _Float16* ap16 = (_Float16*)apack;
+    const int64_t total = P.nct * 64;
+    hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                       cand, P.nc, P.d, P.KS16, P.nct, ap16, cmax);
+    MEPOL_CHECK_LAUNCH();
+    dim3 g((unsigned)((P.nqt + 3) / 4), (unsigned)P.split);
+    switch (P.KS16) {
+      case 1: launch_select16_ks<1>(P, g, ap16, query, cmax, lv, li, st); break;
+      case 2: launch_select16_ks<2>(P, g, ap16, query, cmax, lv, li, st); break;
+      case 3: launch_select16_ks<3>(P, g, ap16, query, cmax, lv, li, st); break;
+      default: launch_select16_ks<4>(P, g, ap16, query, cmax, lv, li, st); break;
+    }
+    MEPOL_CHECK_LAUNCH();
+  } else {
     const int64_t total = P.nct * 64;
     hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, cand,
                        P.nc, P.d, P.KSP, P.nct, apack, cmax);
     MEPOL_CHECK_LAUNCH();
-  }
-  {
     dim3 g((unsigned)((P.nqt + 3) / 4), (unsigned)P.split);
     switch (P.KS) {
       case 2: launch_select_ks<2>(P, g, apack, query, lv, li, st); break;
