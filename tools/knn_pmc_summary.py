@@ -17,11 +17,17 @@ def per_call(db, counter):
     c = sqlite3.connect(db)
     rows = c.execute("select dispatch_id, kernel_name, value from counters_collection "
                      "where counter_name=? order by dispatch_id", (counter,)).fetchall()
-    knn = [(d, n, v) for d, n, v in rows if "mepol::knn::" in n]
-    # A call starts at each pack kernel; keep the last call.
-    starts = [i for i, (_, n, _) in enumerate(knn) if "pack_kernel" in n]
-    last = knn[starts[-1]:]
-    return {n.split("(")[0]: v * 1024.0 for _, n, v in last}
+    knn = [(d, n, v) for d, n, v in rows if "mepol::knn::" in n or "mepol3knn" in n]
+    # A call starts at its first norms kernel (split-f16 path) or at pack_kernel (f32 path);
+    # keep the last call and sum repeated kernels (two norms passes).
+    starts = [i for i, (_, n, _) in enumerate(knn)
+              if "pack_kernel" in n and "pack16" not in n
+              or ("norms_kernel" in n and (i == 0 or "norms_kernel" not in knn[i - 1][1]))]
+    out = {}
+    for _, n, v in knn[starts[-1]:]:
+        key = n.split("(")[0]
+        out[key] = out.get(key, 0.0) + v * 1024.0
+    return out
 
 
 def main(src="gpurun_out"):
