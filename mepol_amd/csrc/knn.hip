@@ -106,7 +106,8 @@ __device__ __forceinline__ void list_insert(float (&ld)[LIST], int (&li)[LIST], 
 // partner lane (l ^ 32 serves the same query column).  Every lane of the wave calls it.
 template <int LIST>
 __device__ __forceinline__ void flush_buffer(float (&ld)[LIST], int (&li)[LIST], float& thr, int& cnt,
-                                             const float (*bv)[64], const int (*bi)[64], int l) {
+                                             const float (*bv)[64], const int (*bi)[64], int l,
+                                             float thr0) {
   const int mc = wave_max_i(cnt);
 #pragma nounroll
   for (int e = 0; e < mc; ++e) {
@@ -121,8 +122,9 @@ __device__ __forceinline__ void flush_buffer(float (&ld)[LIST], int (&li)[LIST],
   }
   cnt = 0;
   // lanes l and l^32 serve the same query: the tighter of their maxima is a valid prune bound
-  // for both (refine's certification bound is the min over all partial-list maxima).
-  thr = fminf(ld[LIST - 1], __shfl_xor(ld[LIST - 1], 32, kWave));
+  // for both (refine's certification bound is the min over all partial-list maxima and the
+  // query's sampled bound thr0).
+  thr = fminf(thr0, fminf(ld[LIST - 1], __shfl_xor(ld[LIST - 1], 32, kWave)));
 }
 
 // Row (candidate within the tile) of accumulator register r for lane l (32x32 C/D map).
@@ -167,7 +169,8 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ a
     ld[j] = INFINITY;
     li[j] = -1;
   }
-  float thr = INFINITY;
+  const float thr0 = INFINITY;
+  float thr = thr0;
   int cnt = 0;
 
   const int64_t t0 = (int64_t)sp * tiles_per_split;
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ a
           ++cnt;
         }
       }
-      if (__ballot(cnt > kBufCap - 16)) flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l);
+      if (__ballot(cnt > kBufCap - 16)) flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0);
     }
   };
   if (t0 < t1) {
@@ -244,7 +247,7 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ a
     wait_all(A0);
     if (t < t1) tile(A0, t);
   }
-  flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l);
+  flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0);
 
   if (qvalid) {
     const int64_t o = ((q * split + sp) * 2 + h) * LIST;
@@ -289,6 +292,14 @@ __device__ __forceinline__ float knn_scale(const unsigned* __restrict__ scal) {
   (void)frexpf(127.9f / m, &e);
   e = max(-100, min(100, e - 1));
   return ldexpf(1.f, e);
+}
+
+// Smallest float above v (v itself for +inf / NaN).
+__device__ __forceinline__ float next_up(float v) {
+  if (!(v < INFINITY)) return v;
+  if (v == 0.f) return __uint_as_float(1u);
+  const unsigned b = __float_as_uint(v);
+  return __uint_as_float(v > 0.f ? b + 1u : b - 1u);
 }
 
 __device__ __forceinline__ void split_f16(float v, _Float16& hi, _Float16& lo) {
@@ -341,20 +352,35 @@ __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X
   }
 }
 
-template <int KS16, int LIST>
+// TAU = false: partial top-LIST lists of every query over its split's tile range, pruned from the
+//              start by the query's sampled bound tau_in (scaled units; nullptr = none).
+// TAU = true : the sampling pass.  Tiles t*tile_stride (t < nct) only, split = 1; writes
+//              tau_out[q] = the next float above min over the two half-lists of their kp1-th
+//              value: an upper bound on the query's (k+1)-th smallest approximate value over all
+//              candidates (a subset's (k+1)-th is never below the full set's), at least kp1
+//              sampled candidates lie at or below it, and the values are bitwise those of the
+//              main pass (same fragments, same MFMA chain).
+template <int KS16, int LIST, bool TAU>
 __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restrict__ apack,
                                                        const float* __restrict__ query,
                                                        int64_t nq, int d, int64_t nct, int split,
-                                                       int64_t tiles_per_split,
-                                                       const unsigned* __restrict__ scal,
+                                                       int64_t tiles_per_split, int tile_stride,
+                                                       int kp1, const unsigned* __restrict__ scal,
+                                                       const float* __restrict__ tau_in,
+                                                       float* __restrict__ tau_out,
                                                        float* __restrict__ out_v,
                                                        int* __restrict__ out_i) {
   __shared__ float sbuf_v[4][kBufCap][64];
   __shared__ int sbuf_i[4][kBufCap][64];
   const int w = threadIdx.x >> 6;
   const int l = threadIdx.x & 63;
-  const int64_t qt = (int64_t)blockIdx.x * 4 + w;
-  const int sp = blockIdx.y;
+  // XCD-aware block mapping: workgroups go round-robin over the 8 XCDs by linear id, so with
+  // sp = id % split (split a multiple of 8) every XCD only ever reads the candidate ranges
+  // sp = xcd (mod 8), which then stay resident in that XCD's 4 MB L2 instead of streaming from
+  // the Infinity Cache once per query tile.
+  const int64_t lin = (int64_t)blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  const int sp = (int)(lin % split);
+  const int64_t qt = (lin / split) * 4 + w;
   if (qt * 32 >= nq) return;  // wave-uniform
   const int h = l >> 5;
   const int64_t q = qt * 32 + (l & 31);
@@ -375,6 +401,7 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
       bhi[s][j] = a;
       blo[s][j] = b;
     }
+  float thr0 = (!TAU && tau_in && qvalid) ? tau_in[q] : INFINITY;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
   for (int s = 0; s < KS16; ++s) {
@@ -384,6 +411,7 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
     bhi[s] = __builtin_bit_cast(f16x8, x);
     blo[s] = __builtin_bit_cast(f16x8, y);
   }
+  asm volatile("" : "+v"(thr0));  // retired above (see filter16_kernel)
 
   float ld[LIST];
   int li[LIST];
@@ -392,7 +420,7 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
     ld[j] = INFINITY;
     li[j] = -1;
   }
-  float thr = INFINITY;
+  float thr = thr0;
   int cnt = 0;
 
   const int64_t t0 = (int64_t)sp * tiles_per_split;
@@ -406,7 +434,7 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
   const f32x4* abase = reinterpret_cast<const f32x4*>(apack) + (int64_t)l * NV;
   f32x4 Bf[3][NV];
   auto load = [&](f32x4 (&A)[NV], int64_t t) {
-    const f32x4* p = abase + t * 64 * NV;
+    const f32x4* p = abase + t * tile_stride * 64 * NV;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       f32x4 x;
@@ -441,7 +469,7 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
     m = fminf(m, fminf(fminf(fminf(acc[8], acc[9]), fminf(acc[10], acc[11])),
                        fminf(fminf(acc[12], acc[13]), fminf(acc[14], acc[15]))));
     if (__ballot(m < thr)) {
-      const int base = (int)(t * 32);
+      const int base = (int)(t * tile_stride * 32);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         if (acc[r] < thr) {
@@ -450,7 +478,7 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
           ++cnt;
         }
       }
-      if (__ballot(cnt > kBufCap - 16)) flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l);
+      if (__ballot(cnt > kBufCap - 16)) flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0);
     }
   };
   if (t0 < t1) {
@@ -492,8 +520,19 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
       for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[b][v]));
     process(accP, t - 1);
   }
-  flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l);
+  flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0);
 
+  if (TAU) {
+    // each half keeps its m = ceil(kp1/2) smallest; the union then holds 2m >= kp1 sampled
+    // values <= max of the two m-th values, a bound about as tight as the union's kp1-th
+    const int m = (kp1 + 1) / 2;
+    float v = INFINITY;
+#pragma unroll
+    for (int j = 0; j < LIST; ++j) v = (j == m - 1) ? ld[j] : v;
+    v = fmaxf(v, __shfl_xor(v, 32, kWave));
+    if (qvalid && h == 0) tau_out[q] = next_up(v);
+    return;
+  }
   if (qvalid) {
     const int64_t o = ((q * split + sp) * 2 + h) * LIST;
 #pragma unroll
@@ -502,6 +541,172 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
       out_i[o + j] = li[j];
     }
   }
+}
+
+// 2c. filter pass (split-f16, seeded by the sampling pass): no sorted lists at all.  Every
+//     candidate whose approximate value is below the query's sampled bound tau (scaled units) is
+//     appended to a per-lane LDS buffer; full buffers are spilled to the query's survivor array
+//     (capacity cap, global count per query; entries past cap only raise the count, which makes
+//     refine queue the query for the exhaustive path).  The tile loop is MFMA chain + min tree +
+//     one compare per tile; with no lists in registers the accumulators stay in VGPRs.
+template <int KS16>
+__global__ __launch_bounds__(256) void filter16_kernel(const _Float16* __restrict__ apack,
+                                                       const float* __restrict__ query,
+                                                       int64_t nq, int d, int64_t nct, int split,
+                                                       int64_t tiles_per_split,
+                                                       const unsigned* __restrict__ scal,
+                                                       const float* __restrict__ tau, int cap,
+                                                       int* __restrict__ counts,
+                                                       float* __restrict__ sv,
+                                                       int* __restrict__ si) {
+  __shared__ float sbuf_v[4][kBufCap][64];
+  __shared__ int sbuf_i[4][kBufCap][64];
+  const int w = threadIdx.x >> 6;
+  const int l = threadIdx.x & 63;
+  // XCD-aware block mapping (see select16_kernel)
+  const int64_t lin = (int64_t)blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
+  const int sp = (int)(lin % split);
+  const int64_t qt = (lin / split) * 4 + w;
+  if (qt * 32 >= nq) return;  // wave-uniform
+  const int h = l >> 5;
+  const int64_t q = qt * 32 + (l & 31);
+  const bool qvalid = q < nq;
+  const float sg = knn_scale(scal);
+  const float inv_s2 = 1.f / (sg * sg);
+
+  f16x8 bhi[KS16], blo[KS16];
+#pragma unroll
+  for (int s = 0; s < KS16; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * s + 8 * h + j;
+      const float v = qvalid ? ((f < d) ? sg * query[q * d + f] : ((f == d) ? 1.f : 0.f)) : 0.f;
+      _Float16 a, b;
+      split_f16(v, a, b);
+      bhi[s][j] = a;
+      blo[s][j] = b;
+    }
+  float thr = qvalid ? tau[q] : -INFINITY;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int s = 0; s < KS16; ++s) {
+    f32x4 x = __builtin_bit_cast(f32x4, bhi[s]);
+    f32x4 y = __builtin_bit_cast(f32x4, blo[s]);
+    asm volatile("" : "+v"(x), "+v"(y));
+    bhi[s] = __builtin_bit_cast(f16x8, x);
+    blo[s] = __builtin_bit_cast(f16x8, y);
+  }
+  // retired by the wait above: no compiler-tracked load may reach the loop (it would drain
+  // vmcnt(0) at the first use in every iteration and serialise the fragment pipeline)
+  asm volatile("" : "+v"(thr));
+  int cnt = 0;
+  const int64_t t0 = (int64_t)sp * tiles_per_split;
+  const int64_t t1 = min(nct, t0 + tiles_per_split);
+
+  constexpr int NV = 2 * KS16;
+  const f32x4* abase = reinterpret_cast<const f32x4*>(apack) + (int64_t)l * NV;
+  f32x4 Bf[3][NV];
+  auto load = [&](f32x4 (&A)[NV], int64_t t) {
+    const f32x4* p = abase + t * 64 * NV;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      f32x4 x;
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(p + v) : "memory");
+      A[v] = x;
+    }
+  };
+  auto landed = [&](f32x4 (&A)[NV]) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV) : "memory");
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      f32x4 x = A[v];
+      asm volatile("" : "+v"(x));
+      A[v] = x;
+    }
+  };
+  auto chain = [&](const f32x4 (&A)[NV]) -> f32x16 {
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < KS16; ++s) {
+      const f16x8 ah = __builtin_bit_cast(f16x8, A[2 * s]);
+      const f16x8 al = __builtin_bit_cast(f16x8, A[2 * s + 1]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bhi[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, blo[s], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bhi[s], acc, 0, 0, 0);
+    }
+    return acc;
+  };
+  // Spill this lane's buffer to the query's survivor array.  The returning atomic makes the
+  // compiler drain vmcnt, which also retires the in-flight fragment loads (correct, and rare).
+  auto spill = [&]() {
+    if (cnt > 0) {
+      const int base = atomicAdd(counts + q, cnt);
+      for (int e = 0; e < cnt; ++e) {
+        const int pos = base + e;
+        if (pos < cap) {
+          sv[q * cap + pos] = sbuf_v[w][e][l] * inv_s2;
+          si[q * cap + pos] = sbuf_i[w][e][l];
+        }
+      }
+    }
+    cnt = 0;
+    // vmcnt(0) here, visible to the compiler: its stores are complete on this rare path, so
+    // the loop latch needs no drain of its own (which would serialise every tile's loads)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+  };
+  auto process = [&](f32x16 acc, int64_t t) {
+    const float m = fminf(
+        fminf(fminf(fminf(acc[0], acc[1]), fminf(acc[2], acc[3])),
+              fminf(fminf(acc[4], acc[5]), fminf(acc[6], acc[7]))),
+        fminf(fminf(fminf(acc[8], acc[9]), fminf(acc[10], acc[11])),
+              fminf(fminf(acc[12], acc[13]), fminf(acc[14], acc[15]))));
+    if (__ballot(m < thr)) {
+      const int base = (int)(t * 32);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (acc[r] < thr) {
+          sbuf_v[w][cnt][l] = acc[r];
+          sbuf_i[w][cnt][l] = base + acc_row(r, l);
+          ++cnt;
+        }
+      }
+      if (__ballot(cnt > kBufCap - 16)) spill();
+    }
+  };
+  if (t0 < t1) {
+    const int64_t tl = t1 - 1;
+    load(Bf[0], t0);
+    load(Bf[1], min(t0 + 1, tl));
+    landed(Bf[0]);
+    f32x16 accP = chain(Bf[0]);
+    load(Bf[2], min(t0 + 2, tl));
+    int64_t t = t0 + 1;
+#define MEPOL_FLT16_STEP(CUR, PREV)         \
+  {                                         \
+    landed(Bf[CUR]);                        \
+    const f32x16 accN = chain(Bf[CUR]);     \
+    process(accP, t - 1);                   \
+    load(Bf[PREV], min(t + 2, tl));         \
+    accP = accN;                            \
+    ++t;                                    \
+  }
+#pragma nounroll
+    while (t + 2 < t1) {
+      MEPOL_FLT16_STEP(1, 0)
+      MEPOL_FLT16_STEP(2, 1)
+      MEPOL_FLT16_STEP(0, 2)
+    }
+    if (t < t1) MEPOL_FLT16_STEP(1, 0)
+    if (t < t1) MEPOL_FLT16_STEP(2, 1)
+#undef MEPOL_FLT16_STEP
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int b = 0; b < 3; ++b)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[b][v]));
+    process(accP, t - 1);
+  }
+  spill();
 }
 
 // ---------------------------------------------------------------------------------------
@@ -542,8 +747,10 @@ __device__ __forceinline__ double sqrt_rn(double x) {
 template <int LIST, int MAXP>
 __global__ __launch_bounds__(256) void refine_kernel(
     const float* __restrict__ cand, int64_t nc, const float* __restrict__ query, int64_t nq, int d,
-    int kp1, int split, const float* __restrict__ lists_v, const int* __restrict__ lists_i,
-    const unsigned* __restrict__ cmax_bits, int e_terms, double* __restrict__ Dout,
+    int kp1, int M, int list_len, const int* __restrict__ counts,
+    const float* __restrict__ lists_v, const int* __restrict__ lists_i,
+    const unsigned* __restrict__ cmax_bits, int e_terms, const float* __restrict__ tau,
+    double* __restrict__ Dout,
     int64_t* __restrict__ I64, int32_t* __restrict__ I32, int* __restrict__ flag_count,
     int* __restrict__ flag_list) {
   __shared__ int sel[4][64];
@@ -551,13 +758,23 @@ __global__ __launch_bounds__(256) void refine_kernel(
   const int l = threadIdx.x & 63;
   const int64_t q = (int64_t)blockIdx.x * 4 + w;
   if (q >= nq) return;
-  const int M = 2 * split * LIST;
+  // Candidate entries of this query: M per query.  Lists mode (counts == nullptr): 2*split
+  // ascending partial lists of list_len each.  Survivor mode: counts[q] unsorted entries (a count
+  // above M means entries were dropped: the query is not certified).
   const float* lv = lists_v + q * M;
   const int* lix = lists_i + q * M;
+  const int nval = counts ? min(counts[q], M) : M;
+  const bool overflow = counts && counts[q] > M;
 
-  // Bound part 1: min over partial lists of their maxima (last, lists are ascending).
+  // Bound part 1: min over partial lists of their maxima (last, lists are ascending) and the
+  // sampled bound the selection started from (scaled units -> unscaled, exact power of two).
   float bnd = INFINITY;
-  for (int p = l; p < 2 * split; p += 64) bnd = fminf(bnd, lv[p * LIST + LIST - 1]);
+  if (tau) {
+    const float sg = knn_scale(cmax_bits);
+    bnd = tau[q] / (sg * sg);
+  }
+  if (list_len > 0)
+    for (int p = l; p < M / list_len; p += 64) bnd = fminf(bnd, lv[p * list_len + list_len - 1]);
 
   float ev[MAXP];
   int ei[MAXP];
@@ -566,7 +783,7 @@ __global__ __launch_bounds__(256) void refine_kernel(
     const int e = p * 64 + l;
     float v = INFINITY;
     int ix = INT_MAX;
-    if (e < M) {
+    if (e < nval) {
       const int ii = lix[e];
       if (ii >= 0 && ii < nc) {
         v = lv[e];
@@ -648,7 +865,7 @@ __global__ __launch_bounds__(256) void refine_kernel(
                        (cmax * cmax + 2.0 * cmax * sqrt(qn2)) + 1e-300;
   const double ek = __shfl(dd, kp1 - 1, kWave);
   const int eki = __shfl(di, kp1 - 1, kWave);
-  bool ok = (eki != INT_MAX);
+  bool ok = (eki != INT_MAX) && !overflow;
   if (bnd < 1e29f) ok = ok && (ek < ((double)bnd + qn2) - E);
   if (l < kp1) {
     Dout[q * kp1 + l] = sqrt_rn(dd);
@@ -765,8 +982,13 @@ struct Plan {
   int mode;       // 0: f32 MFMA selection, 1: split-f16 MFMA selection (default, d + 1 <= 64)
   int KS16;       // k-steps of 16 (mode 1)
   int e_terms;    // selection error bound multiplier (refine certification)
+  int sample;     // mode 1: tile stride of the sampling pass that seeds each query's bound (0: off)
+  int filter;     // mode 1 + sampling: survivor filter pass (filter16_kernel) instead of lists
+  int tau_list;   // list length of the sampling pass: >= ceil(kp1 / 2)
+  int M;          // refine input entries per query (lists: 2*split*LIST; filter: capacity)
+  int list_len;   // refine: length of each ascending partial list (0: unsorted survivors)
   int64_t nc, nq, nct, nqt, tiles_per_split;
-  size_t off_apack, off_scalars, off_lv, off_li, off_flag, total;
+  size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_tau, off_cnt, total;
 };
 
 static const int kKSChoices[] = {2, 4, 8, 12, 15, 16, 24, 32};
@@ -818,6 +1040,22 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
     // f32: d + 1 fma-chain roundings, x4 margin.  split-f16: 3 K products per output summed in
     // f32 (<= 3K roundings), operand splitting 3 * 2^-22 = 12 * 2^-24, |c|^2 in f32 (d), x2.
     P->e_terms = P->mode ? 2 * (3 * 16 * P->KS16 + 16 + d) : 4 * (d + 1);
+    // Sampling pass: every S-th candidate tile (MEPOL_KNN_SAMPLE=S, off by default: at C3 the
+    // survivor filter measured slower than the list selection); only worth it when the sample
+    // still holds many tiles.
+    const char* smp = getenv("MEPOL_KNN_SAMPLE");
+    int S = smp ? atoi(smp) : 0;
+    const int64_t nct = (nc + 31) / 32;
+    if (S < 2 || P->mode != 1 || nct / S < 8 || (int64_t)32 * (nct / S) < 4 * kp1) S = 0;
+    P->sample = S;
+    P->tau_list = 64;
+    for (int v : kListChoices)
+      if (v >= (kp1 + 1) / 2) {
+        P->tau_list = v;
+        break;
+      }
+    const char* flt = getenv("MEPOL_KNN_FILTER");
+    P->filter = (S > 0 && !(flt && flt[0] == '0')) ? 1 : 0;
   }
   P->KS = KS;
   P->KSP = (KS + 3) / 4 * 4;
@@ -827,7 +1065,12 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   P->nct = (nc + 31) / 32;
   P->nqt = (nq + 31) / 32;
   int split = split_hint;
-  if (split <= 0) {
+  if (split <= 0 && P->mode == 1 && P->filter) {
+    // filter pass: 8 candidate ranges, one per XCD (filter16's block mapping), each small
+    // enough for that XCD's L2 (25.6 MB of fragments at C3 -> 3.2 MB per XCD)
+    split = 8;
+    while (split > 1 && P->nct / split < 16) split >>= 1;
+  } else if (split <= 0) {
     // enough waves to fill 256 CUs x ~3 waves/SIMD several times over, tiles >= 16 per split
     const int64_t target = 16384;
     split = (int)std::min<int64_t>(kMaxSplit, std::max<int64_t>(1, (target + P->nqt - 1) / std::max<int64_t>(P->nqt, 1)));
@@ -836,7 +1079,22 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   split = std::max(1, std::min(split, kMaxSplit));
   P->split = split;
   P->tiles_per_split = (P->nct + split - 1) / split;
-  P->maxp = (2 * split * LIST + 63) / 64;
+  if (P->filter) {
+    // survivors of the sampled bound: ~S*kp1 expected per query (S = 16 -> ~500 at k+1 = 31),
+    // capacity 32*kp1 (>= 256); an overflowing query is answered by the exhaustive path
+    const char* capv = getenv("MEPOL_KNN_CAP");
+    const int cap = capv ? atoi(capv) : 32 * kp1;
+    P->M = (int)align_up((size_t)std::max(256, std::min(cap, 2048)), 64);
+    P->list_len = 0;
+  } else {
+    P->M = 2 * split * LIST;
+    P->list_len = LIST;
+  }
+  P->maxp = (P->M + 63) / 64;
+  if (P->maxp > 32) {
+    set_error("mepol_knn: refine capacity %d entries per query exceeds 2048", P->M);
+    return kErrUnsupported;
+  }
   size_t off = 0;
   P->off_apack = off;
   off = align_up(off + std::max((size_t)P->nct * 64 * P->KSP * sizeof(float),
@@ -844,12 +1102,16 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
                  256);
   P->off_scalars = off;
   off = align_up(off + 16, 256);
-  const size_t nl = (size_t)std::max<int64_t>(nq, 1) * 2 * split * LIST;
+  const size_t nl = (size_t)std::max<int64_t>(nq, 1) * P->M;
   P->off_lv = off;
   off = align_up(off + nl * sizeof(float), 256);
   P->off_li = off;
   off = align_up(off + nl * sizeof(int), 256);
   P->off_flag = off;
+  off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(int), 256);
+  P->off_tau = off;
+  off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(float), 256);
+  P->off_cnt = off;
   off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(int), 256);
   P->total = off;
   return 0;
@@ -879,13 +1141,25 @@ static void launch_select_ks(const Plan& P, dim3 g, const float* ap, const float
   }
 }
 
+// tau_pass: the sampling pass (split 1, every P.sample-th tile) writing tau; otherwise the main
+// selection, seeded by tau when it is non-null.
 template <int KS16>
-static void launch_select16_ks(const Plan& P, dim3 g, const _Float16* ap, const float* query,
-                               const unsigned* scal, float* lv, int* li, hipStream_t st) {
-#define MEPOL_SEL16(L)                                                                          \
-  hipLaunchKernelGGL((select16_kernel<KS16, L>), g, dim3(256), 0, st, ap, query, P.nq, P.d, P.nct, \
-                     P.split, P.tiles_per_split, scal, lv, li)
-  switch (P.LIST) {
+static void launch_select16_ks(const Plan& P, const _Float16* ap, const float* query,
+                               const unsigned* scal, float* tau, bool tau_pass, float* lv, int* li,
+                               hipStream_t st) {
+  const unsigned gx = (unsigned)((P.nqt + 3) / 4);
+#define MEPOL_SEL16(L)                                                                            \
+  if (tau_pass) {                                                                                 \
+    const int64_t ns = (P.nct + P.sample - 1) / P.sample;                                         \
+    hipLaunchKernelGGL((select16_kernel<KS16, L, true>), dim3(gx, 1), dim3(256), 0, st, ap, query, \
+                       P.nq, P.d, ns, 1, ns, P.sample, P.kp1, scal, nullptr, tau, nullptr,         \
+                       nullptr);                                                                  \
+  } else {                                                                                        \
+    hipLaunchKernelGGL((select16_kernel<KS16, L, false>), dim3(gx, (unsigned)P.split), dim3(256), \
+                       0, st, ap, query, P.nq, P.d, P.nct, P.split, P.tiles_per_split, 1, P.kp1,  \
+                       scal, tau, nullptr, lv, li);                                               \
+  }
+  switch (tau_pass ? P.tau_list : P.LIST) {
     case 8: MEPOL_SEL16(8); break;
     case 16: MEPOL_SEL16(16); break;
     case 40: MEPOL_SEL16(40); break;
@@ -896,25 +1170,26 @@ static void launch_select16_ks(const Plan& P, dim3 g, const _Float16* ap, const 
 
 template <int LIST>
 static void launch_refine_list(const Plan& P, const float* cand, const float* query,
-                               const float* lv, const int* li, const unsigned* cmax, double* D,
-                               int64_t* I64, int32_t* I32, int* fc, int* fl, hipStream_t st) {
+                               const float* lv, const int* li, const unsigned* cmax,
+                               const float* tau, const int* counts, double* D, int64_t* I64,
+                               int32_t* I32, int* fc, int* fl, hipStream_t st) {
   dim3 g((unsigned)((P.nq + 3) / 4));
-  // MAXP = ceil(2 * split * LIST / 64) for split <= kMaxSplit
+  // MAXP = ceil(M / 64) <= 32
   if (P.maxp <= 2)
     hipLaunchKernelGGL((refine_kernel<LIST, 2>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.split, lv, li, cmax, P.e_terms, D, I64, I32, fc, fl);
+                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl);
   else if (P.maxp <= 4)
     hipLaunchKernelGGL((refine_kernel<LIST, 4>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.split, lv, li, cmax, P.e_terms, D, I64, I32, fc, fl);
+                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl);
   else if (P.maxp <= 8)
     hipLaunchKernelGGL((refine_kernel<LIST, 8>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.split, lv, li, cmax, P.e_terms, D, I64, I32, fc, fl);
+                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl);
   else if (P.maxp <= 16)
     hipLaunchKernelGGL((refine_kernel<LIST, 16>), g, dim3(256), 0, st, cand, P.nc, query, P.nq,
-                       P.d, P.kp1, P.split, lv, li, cmax, P.e_terms, D, I64, I32, fc, fl);
+                       P.d, P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl);
   else
     hipLaunchKernelGGL((refine_kernel<LIST, 32>), g, dim3(256), 0, st, cand, P.nc, query, P.nq,
-                       P.d, P.kp1, P.split, lv, li, cmax, P.e_terms, D, I64, I32, fc, fl);
+                       P.d, P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl);
 }
 
 template <int LIST>
@@ -976,6 +1251,8 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
   int* li = (int*)(ws + P.off_li);
   int* flist = (int*)(ws + P.off_flag);
 
+  float* tau = nullptr;   // sampled per-query bounds (mode 1 with sampling)
+  int* counts = nullptr;  // survivors per query (filter pass)
   MEPOL_HIP(hipMemsetAsync(ws + P.off_scalars, 0, 16, st));
   if (n_fallback_out) MEPOL_HIP(hipMemsetAsync(n_fallback_out, 0, sizeof(int32_t), st));
   if (P.mode == 1) {
@@ -989,14 +1266,35 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
     hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                        cand, P.nc, P.d, P.KS16, P.nct, ap16, cmax);
     MEPOL_CHECK_LAUNCH();
-    dim3 g((unsigned)((P.nqt + 3) / 4), (unsigned)P.split);
-    switch (P.KS16) {
-      case 1: launch_select16_ks<1>(P, g, ap16, query, cmax, lv, li, st); break;
-      case 2: launch_select16_ks<2>(P, g, ap16, query, cmax, lv, li, st); break;
-      case 3: launch_select16_ks<3>(P, g, ap16, query, cmax, lv, li, st); break;
-      default: launch_select16_ks<4>(P, g, ap16, query, cmax, lv, li, st); break;
+    tau = P.sample ? (float*)(ws + P.off_tau) : nullptr;
+    if (P.filter) {
+      counts = (int*)(ws + P.off_cnt);
+      MEPOL_HIP(hipMemsetAsync(counts, 0, (size_t)P.nq * sizeof(int), st));
     }
-    MEPOL_CHECK_LAUNCH();
+    for (int pass = tau ? 0 : 1; pass < 2; ++pass) {
+      if (pass == 1 && P.filter) {
+        const dim3 g((unsigned)((P.nqt + 3) / 4), (unsigned)P.split);
+#define MEPOL_FLT16(K)                                                                          \
+  hipLaunchKernelGGL((filter16_kernel<K>), g, dim3(256), 0, st, ap16, query, P.nq, P.d, P.nct,  \
+                     P.split, P.tiles_per_split, cmax, tau, P.M, counts, lv, li)
+        switch (P.KS16) {
+          case 1: MEPOL_FLT16(1); break;
+          case 2: MEPOL_FLT16(2); break;
+          case 3: MEPOL_FLT16(3); break;
+          default: MEPOL_FLT16(4); break;
+        }
+#undef MEPOL_FLT16
+        MEPOL_CHECK_LAUNCH();
+        continue;
+      }
+      switch (P.KS16) {
+        case 1: launch_select16_ks<1>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
+        case 2: launch_select16_ks<2>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
+        case 3: launch_select16_ks<3>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
+        default: launch_select16_ks<4>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
+      }
+      MEPOL_CHECK_LAUNCH();
+    }
   } else {
     const int64_t total = P.nct * 64;
     hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, cand,
@@ -1016,10 +1314,10 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
     MEPOL_CHECK_LAUNCH();
   }
   switch (P.LIST) {
-    case 8: launch_refine_list<8>(P, cand, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st); break;
-    case 16: launch_refine_list<16>(P, cand, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st); break;
-    case 40: launch_refine_list<40>(P, cand, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st); break;
-    default: launch_refine_list<64>(P, cand, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st); break;
+    case 8: launch_refine_list<8>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
+    case 16: launch_refine_list<16>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
+    case 40: launch_refine_list<40>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
+    default: launch_refine_list<64>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
   }
   MEPOL_CHECK_LAUNCH();
   const unsigned eg = 512;
