@@ -41,13 +41,16 @@ def _batched_kind(env):
     return getattr(type(unwrap(env)), "batched_kind", None)
 
 
-def collect_particles_device(env, policy, num_traj, traj_len, state_filter, generator=None):
+def collect_particles_device(env, policy, num_traj, traj_len, state_filter, generator=None,
+                             visited=None):
     """Rollout of num_traj trajectories of traj_len steps, batched on the policy's device.
 
     Returns device tensors: states f32 [nt, T+1, nf], actions f32 [nt, T, a], real lengths
     int32 [nt, 1], next_states f32 [N, ns] (particle p = n*T + t <-> s_{n, t+1}, mepol.py:98-109).
     MountainCar / GridWorld step in a HIP kernel (one fused launch per step after the MLP);
     any other env is stepped on the host in lockstep with one batched policy call per step.
+    `visited` (optional, f64 [nt, T, nf]) receives the env's own state after every step (f64
+    MountainCar state / GridWorld f32 state, not the f32 particle copy), for the heatmap.
     """
     dev = policy.device
     if dev.type != "cuda":
@@ -74,6 +77,8 @@ def collect_particles_device(env, policy, num_traj, traj_len, state_filter, gene
                                     generator=generator)
                 ops.rollout_step(env_id, env64, env32, mean, noise, log_std, t, T, states, actions,
                                  policy_in)
+                if visited is not None:
+                    visited[:, t].copy_(policy_in)
         else:
             envs = [env] + [_clone_env(env) for _ in range(num_traj - 1)]
             s = np.stack([e.reset() for e in envs])
@@ -85,11 +90,62 @@ def collect_particles_device(env, policy, num_traj, traj_len, state_filter, gene
                 a_np = a.cpu().numpy()
                 s = np.stack([e.step(a_np[i])[0] for i, e in enumerate(envs)])
                 states[:, t + 1] = torch.as_tensor(s, dtype=torch.float32, device=dev)
+                if visited is not None:
+                    visited[:, t] = torch.as_tensor(s, dtype=torch.float64, device=dev)
     rtl = torch.full((num_traj, 1), T, dtype=torch.int32, device=dev)
     next_states = states[:, 1:, :].reshape(-1, nf)
     if state_filter is not None:
         next_states = next_states[:, list(state_filter)]
     return states, actions, rtl, next_states.contiguous()
+
+
+def get_heatmap(env, policy, discretizer, num_episodes, num_steps, cmap, interp, labels):
+    """State-visitation heatmap of the policy (mepol.py:19-67), all episodes in one rollout.
+
+    The reference runs num_episodes episodes of num_steps steps one after another and stops an
+    episode on `done`; every MEPOL env is wrapped in ErgodicEnv (done is always False), so each
+    episode is exactly num_steps steps and the episodes are the trajectories of one batched
+    collect_particles_device call.  The visited states are recorded in f64 and binned on the
+    device (Discretizer.visitation_stats, np.digitize semantics).  Returns
+    (average_state_dist ndarray [bins], average_entropy float, figure; None without matplotlib).
+    """
+    nf = env.num_features
+    visited = torch.empty((num_episodes, num_steps, nf), dtype=torch.float64,
+                          device=policy.device)
+    collect_particles_device(env, policy, num_episodes, num_steps, None, visited=visited)
+    dist, ent = discretizer.visitation_stats(visited)
+    average_state_dist = dist.cpu().numpy()
+    image = _heatmap_figure(average_state_dist, discretizer.bins_sizes, cmap, interp, labels)
+    return average_state_dist, float(ent), image
+
+
+def _heatmap_figure(average_state_dist, bins_sizes, cmap, interp, labels):
+    """The reference's figure (mepol.py:49-65): log-probability image (2-D) or bar chart."""
+    try:
+        import matplotlib
+
+        matplotlib.use("Agg")
+        import matplotlib.pyplot as plt
+    except Exception:
+        return None
+    plt.close()
+    fig = plt.figure()
+    plt.xticks([])
+    plt.yticks([])
+    if labels is not None:
+        plt.xlabel(labels[0])
+        plt.ylabel(labels[1])
+    if average_state_dist.ndim == 2:
+        log_p = np.ma.log(average_state_dist)
+        flat = log_p.ravel()
+        lo = np.min(flat)
+        rest = flat[flat != lo]
+        if rest.count() > 0:
+            flat[np.argmin(flat)] = np.min(rest)
+        plt.imshow(log_p.filled(lo), interpolation=interp, cmap=cmap)
+    else:
+        plt.bar(list(range(bins_sizes[0])), average_state_dist)
+    return fig
 
 
 def _clone_env(env):
@@ -306,9 +362,15 @@ def log_epoch_statistics(writer, log_file, csv_file_1, csv_file_2, epoch, loss, 
     writer.add_scalar("Number off-policy iteration", num_off_iters, global_step=epoch)
     if full_entropy is not None:
         writer.add_scalar("Full Entropy:", full_entropy, global_step=epoch)
+    # the reference keys the heatmap outputs on the figure (mepol.py:216,230,247); here on the
+    # entropy, so the CSV row is kept when matplotlib is absent
+    if heatmap_image is not None:
+        writer.add_figure("Heatmap", heatmap_image, global_step=epoch)
+    if heatmap_entropy is not None:
+        writer.add_scalar("Discrete entropy", heatmap_entropy, global_step=epoch)
     rows = [["Epoch", epoch], ["Execution time (s)", f"{execution_time:.3f}"],
             ["Entropy", f"{entropy:.3f}"], ["Off-policy iters", num_off_iters]]
-    if heatmap_image is not None:
+    if heatmap_entropy is not None:
         rows.append(["Heatmap entropy", f"{heatmap_entropy:.3f}"])
     if backtrack_iters is not None:
         rows.append(["Backtrack iters", backtrack_iters])
@@ -320,7 +382,7 @@ def log_epoch_statistics(writer, log_file, csv_file_1, csv_file_2, epoch, loss, 
         grid = "\n".join(f"{a}: {b}" for a, b in rows)
     csv_file_1.write(f"{epoch},{loss},{entropy},{full_entropy},{num_off_iters},{execution_time}\n")
     csv_file_1.flush()
-    if heatmap_image is not None and csv_file_2 is not None:
+    if heatmap_entropy is not None and csv_file_2 is not None:
         csv_file_2.write(f"{epoch},{heatmap_entropy}\n")
         csv_file_2.flush()
     log_file.write(grid)
@@ -350,7 +412,8 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
           heatmap_interp, seed, out_path, num_workers):
     """The MEPOL epoch loop (mepol.py:284-545) with the reference's control flow and outputs.
 
-    Heatmaps (mepol.py:19-67) are out of scope: a discretizer is accepted and ignored.
+    Heatmaps (mepol.py:19-67) are computed on the device (get_heatmap) when a discretizer is
+    given, at epoch 0 and every heatmap_every epochs, and logged to {env_name}-heatmap.csv.
     """
     if seed is not None:
         np.random.seed(seed)
@@ -376,7 +439,20 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
     csv_file_1.write(",".join(["epoch", "loss", "entropy", "full_entropy", "num_off_iters",
                                "execution_time"]))
     csv_file_1.write("\n")
-    csv_file_2 = None
+    if heatmap_discretizer is not None:
+        csv_file_2 = open(os.path.join(out_path, f"{env_name}-heatmap.csv"), "w")
+        csv_file_2.write(",".join(["epoch", "average_entropy"]))
+        csv_file_2.write("\n")
+    else:
+        csv_file_2 = None
+
+    def heatmap():
+        if heatmap_discretizer is None:
+            return None, None
+        _, h, image = get_heatmap(env, behavioral_policy, heatmap_discretizer, heatmap_episodes,
+                                  heatmap_num_steps, heatmap_cmap, heatmap_interp, heatmap_labels)
+        return h, image
+
     csv_file_3 = open(os.path.join(out_path, f"{env_name}_off_policy_iter.csv"), "w")
     csv_file_3.write(",".join(["epoch", "off_policy_iter", "entropy", "kl", "learning_rate"]))
     csv_file_3.write("\n")
@@ -406,8 +482,7 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
     entropy = _np(entropy)
     execution_time = time.time() - t0
     loss = -entropy
-    heatmap_entropy = None
-    heatmap_image = None
+    heatmap_entropy, heatmap_image = heatmap()
     _save_policy(behavioral_policy, os.path.join(out_path, f"{epoch}-policy"))
     log_epoch_statistics(writer=writer, log_file=log_file, csv_file_1=csv_file_1,
                          csv_file_2=csv_file_2, epoch=epoch, loss=loss, entropy=entropy,
@@ -450,7 +525,9 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
         entropy = _np(entropy)
         execution_time = time.time() - t0
 
+        heatmap_entropy, heatmap_image = None, None
         if epoch % heatmap_every == 0:
+            heatmap_entropy, heatmap_image = heatmap()
             states, actions, real_traj_lengths, next_states, distances, indices = \
                 collect_particles_and_compute_knn(env, behavioral_policy,
                                                   num_traj * full_entropy_traj_scale, traj_len,
@@ -465,7 +542,8 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
         log_epoch_statistics(writer=writer, log_file=log_file, csv_file_1=csv_file_1,
                              csv_file_2=csv_file_2, epoch=epoch, loss=loss, entropy=entropy,
                              execution_time=execution_time, num_off_iters=num_off_iters,
-                             full_entropy=full_entropy, heatmap_image=None, heatmap_entropy=None,
+                             full_entropy=full_entropy, heatmap_image=heatmap_image,
+                             heatmap_entropy=heatmap_entropy,
                              backtrack_iters=backtrack_iter, backtrack_lr=learning_rate)
     return behavioral_policy
 

@@ -10,7 +10,8 @@ directory layout and log_info.txt.  Runs the hot path on the GPU:
         --zero_mean_start 1 --full_entropy_traj_scale 5 --full_entropy_k 50 --num_workers 1
 
 MuJoCo environments (Ant, AntXY, Humanoid, HumanoidXYZ, HandReach) keep their specs but need
-mujoco-py, which is outside this build's scope; heatmaps are not drawn (logging only).
+mujoco-py, which is outside this build's scope.  Heatmaps are computed on the GPU
+(algorithms/mepol.py::get_heatmap) with the specs' discretizers.
 """
 import argparse
 import os
@@ -69,20 +70,32 @@ def build_parser():
 
 def exp_specs():
     from ..envs import ErgodicEnv, GridWorldContinuous, MountainCarContinuous
+    from ..envs.discretizer import Discretizer
 
+    xy = dict(discretizer_create=lambda env: Discretizer([[-12.0, 12.0], [-12.0, 12.0]], [40, 40],
+                                                         lambda s: [s[0], s[1]]),
+              heatmap_interp="spline16", heatmap_cmap="Blues", heatmap_labels=("X", "Y"))
     mujoco = dict(hidden_sizes=[400, 300], activation=nn.ReLU, log_std_init=-0.5, eps=0,
                   env_create=None)
     return {
         "MountainCar": dict(env_create=lambda: ErgodicEnv(MountainCarContinuous()),
+                            discretizer_create=lambda env: Discretizer(
+                                [[env.min_position, env.max_position],
+                                 [-env.max_speed, env.max_speed]], [12, 11]),
                             hidden_sizes=[300, 300], activation=nn.ReLU, log_std_init=-0.5,
-                            eps=1e-15),
+                            eps=1e-15, heatmap_interp="spline16", heatmap_cmap="Blues",
+                            heatmap_labels=("Position", "Velocity")),
         "GridWorld": dict(env_create=lambda: ErgodicEnv(GridWorldContinuous()),
-                          hidden_sizes=[300, 300], activation=nn.ReLU, log_std_init=-1.5, eps=0),
-        "Ant": dict(mujoco, state_filter=list(range(7))),
-        "AntXY": dict(mujoco, state_filter=list(range(2))),
-        "Humanoid": dict(mujoco, state_filter=list(range(24))),
-        "HumanoidXYZ": dict(mujoco, state_filter=list(range(3))),
-        "HandReach": dict(mujoco, state_filter=list(range(24))),
+                          discretizer_create=lambda env: Discretizer(
+                              [[-env.dim, env.dim], [-env.dim, env.dim]], [20, 20]),
+                          hidden_sizes=[300, 300], activation=nn.ReLU, log_std_init=-1.5, eps=0,
+                          heatmap_interp=None, heatmap_cmap="Blues", heatmap_labels=("X", "-Y")),
+        "Ant": dict(mujoco, **xy, state_filter=list(range(7))),
+        "AntXY": dict(mujoco, **xy, state_filter=list(range(2))),
+        "Humanoid": dict(mujoco, **xy, state_filter=list(range(24))),
+        "HumanoidXYZ": dict(mujoco, **xy, state_filter=list(range(3))),
+        "HandReach": dict(mujoco, discretizer_create=lambda env: None,
+                          state_filter=list(range(24))),
     }
 
 
@@ -148,9 +161,11 @@ def main(argv=None):
           num_epochs=args.num_epochs, optimizer=args.optimizer,
           full_entropy_traj_scale=args.full_entropy_traj_scale,
           full_entropy_k=args.full_entropy_k, heatmap_every=args.heatmap_every,
-          heatmap_discretizer=None, heatmap_episodes=args.heatmap_episodes,
-          heatmap_num_steps=args.heatmap_num_steps, heatmap_cmap=None, heatmap_labels=None,
-          heatmap_interp=None, seed=args.seed, out_path=out_path, num_workers=args.num_workers)
+          heatmap_discretizer=spec["discretizer_create"](env),
+          heatmap_episodes=args.heatmap_episodes, heatmap_num_steps=args.heatmap_num_steps,
+          heatmap_cmap=spec.get("heatmap_cmap"), heatmap_labels=spec.get("heatmap_labels"),
+          heatmap_interp=spec.get("heatmap_interp"), seed=args.seed, out_path=out_path,
+          num_workers=args.num_workers)
     return 0
 
 

@@ -193,6 +193,31 @@ def rollout(env, sd, log_std, init, noise, T):
 
 
 # -------------------------------------------------------------------------------------------
+# Visitation heatmap  (src/algorithms/mepol.py:26-47, src/envs/discretizer.py:4-26)
+# -------------------------------------------------------------------------------------------
+def heatmap_stats(ranges, bins_sizes, visits):
+    """get_heatmap's statistics over recorded visits [E, T, nf] (nf = len(bins_sizes), already
+    the discretized features): per-episode np.digitize bin counts / T, their average, and the
+    average scipy.stats.entropy, accumulated episode by episode as the reference does."""
+    import scipy.stats
+
+    edges = [np.linspace(ranges[i][0], ranges[i][1], bins_sizes[i] + 1)[1:-1]
+             for i in range(len(bins_sizes))]
+    E, T = visits.shape[0], visits.shape[1]
+    avg = np.zeros(bins_sizes)
+    avg_h = 0.0
+    for e in range(E):
+        dist = np.zeros(bins_sizes)
+        for t in range(T):
+            s = visits[e, t]
+            dist[tuple(np.digitize(x=s[i], bins=edges[i]) for i in range(len(s)))] += 1
+        dist /= T
+        avg += dist
+        avg_h += scipy.stats.entropy(dist.ravel())
+    return avg / E, avg_h / E
+
+
+# -------------------------------------------------------------------------------------------
 # Timed CPU baseline: one MEPOL off-policy iteration in the reference's own shape
 # -------------------------------------------------------------------------------------------
 class TorchPolicy(torch.nn.Module):

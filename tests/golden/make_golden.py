@@ -21,6 +21,8 @@ Fixtures:
                    gridworld_continuous.py:128-154), edge cases included.
   control_*.npz    mepol() off-policy control flow (mepol.py:404-499) driven by scripted
                    (loss, KL) sequences: learning rates, accepts, backtracks, CSV rows.
+  heatmap_*.npz    get_heatmap (mepol.py:19-67) + Discretizer (src/envs/discretizer.py) over
+                   scripted visits: average distribution and average discrete entropy.
 """
 import io
 import json
@@ -335,10 +337,63 @@ def gen_control(M, GaussianPolicy, torch):
               trace=np.array(json.dumps(trace)), csv1=np.array(csv1), csv3=np.array(csv3))
 
 
+def gen_heatmap(M):
+    """get_heatmap (mepol.py:19-67) with the reference's Discretizer over scripted visits: a
+    replay env hands back fixed states (30 % exactly on bin edges, some outside the ranges)
+    and the policy's action is ignored, so the fixture pins binning, averaging and entropy."""
+    import matplotlib
+
+    matplotlib.use("Agg")
+    import torch
+    from src.envs.discretizer import Discretizer
+
+    class Replay:
+        def __init__(self, visits):
+            self.visits, self.ep, self.t = visits, -1, 0
+
+        def reset(self):
+            self.ep += 1
+            self.t = 0
+            return np.zeros_like(self.visits[0, 0])
+
+        def step(self, a):
+            s = self.visits[self.ep, self.t]
+            self.t += 1
+            return s, 0.0, False, {}
+
+    class Still:
+        def predict(self, s, deterministic=False):
+            return torch.zeros(1, dtype=torch.float64)
+
+    rng = np.random.default_rng(11)
+    E, T = 6, 250
+    cases = [("mc", [[-1.2, 0.6], [-0.07, 0.07]], [12, 11], 2, False, np.float64),
+             ("gw", [[-6.0, 6.0], [-6.0, 6.0]], [20, 20], 2, False, np.float32),
+             ("xy", [[-12.0, 12.0], [-12.0, 12.0]], [40, 40], 5, True, np.float64)]
+    for name, ranges, bins, nf, xy, dt in cases:
+        cols = []
+        for (lo, hi), nb in zip(ranges, bins):
+            edges = np.linspace(lo, hi, nb + 1)
+            x = rng.uniform(lo - 0.1 * (hi - lo), hi + 0.1 * (hi - lo), E * T)
+            pick = rng.random(E * T) < 0.3
+            x[pick] = rng.choice(edges, int(pick.sum()))
+            cols.append(x)
+        vis = np.stack(cols, 1)
+        if nf > 2:
+            vis = np.concatenate([vis, rng.standard_normal((E * T, nf - 2))], 1)
+        vis = vis.astype(dt).reshape(E, T, nf)
+        disc = Discretizer(ranges, bins, (lambda s: [s[0], s[1]]) if xy else None)
+        dist, ent, _ = M.get_heatmap(Replay(vis), Still(), disc, E, T, "Blues", None, ("X", "Y"))
+        _save(f"heatmap_{name}.npz", visits=vis, ranges=np.array(ranges, np.float64),
+              bins=np.array(bins), xy=np.array(xy), dist=np.asarray(dist, np.float64),
+              entropy=np.array(float(ent)))
+
+
 def main():
     if not os.path.isdir(REF):
         print("reference not present; nothing to do")
         return
+    only = set(sys.argv[1:])  # e.g. `make_golden.py heatmap` regenerates one family
     sys.path.insert(0, HERE)
     import ref_stubs
 
@@ -353,12 +408,19 @@ def main():
     from src.policy import GaussianPolicy, train_supervised
 
     torch.set_num_threads(8)
-    gen_env(GridWorldContinuous, MountainCarContinuous)
-    gen_policy(GaussianPolicy, torch)
-    gen_knn(M, GridWorldContinuous, ErgodicEnv, GaussianPolicy, train_supervised, torch)
-    gen_entropy(M, GridWorldContinuous, MountainCarContinuous, ErgodicEnv, GaussianPolicy,
-                train_supervised, torch, scipy)
-    gen_control(M, GaussianPolicy, torch)
+    if not only or "env" in only:
+        gen_env(GridWorldContinuous, MountainCarContinuous)
+    if not only or "policy" in only:
+        gen_policy(GaussianPolicy, torch)
+    if not only or "knn" in only:
+        gen_knn(M, GridWorldContinuous, ErgodicEnv, GaussianPolicy, train_supervised, torch)
+    if not only or "entropy" in only:
+        gen_entropy(M, GridWorldContinuous, MountainCarContinuous, ErgodicEnv, GaussianPolicy,
+                    train_supervised, torch, scipy)
+    if not only or "control" in only:
+        gen_control(M, GaussianPolicy, torch)
+    if not only or "heatmap" in only:
+        gen_heatmap(M)
 
 
 if __name__ == "__main__":

@@ -36,3 +36,8 @@ def test_cli_epochs(cuda, tmp_path, env, k):
         assert sorted(sd) == ["log_std", "mean.bias", "mean.weight", "net.0.bias", "net.0.weight",
                               "net.2.bias", "net.2.weight"]
     assert os.path.exists(os.path.join(run, "log_info.txt"))
+    # heatmap CSV (mepol.py:325-328, 247-249): epoch 0 and every heatmap_every epochs
+    csv2 = open(os.path.join(run, f"{env}-heatmap.csv")).read().strip().splitlines()
+    assert csv2[0] == "epoch,average_entropy"
+    assert [int(r.split(",")[0]) for r in csv2[1:]] == [0, 2]
+    assert all(float(r.split(",")[1]) >= 0.0 for r in csv2[1:])
