@@ -377,10 +377,13 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
   // XCD-aware block mapping: workgroups go round-robin over the 8 XCDs by linear id, so with
   // sp = id % split (split a multiple of 8) every XCD only ever reads the candidate ranges
   // sp = xcd (mod 8), which then stay resident in that XCD's 4 MB L2 instead of streaming from
-  // the Infinity Cache once per query tile.
+  // the Infinity Cache once per query tile.  Any other split (3 at C3) keeps the split-major
+  // order: the blocks in flight then all read one candidate range, not every range at once
+  // (the XCD mapping with split = 3 put all three ranges in every L2: 2.7x the fetch bytes).
   const int64_t lin = (int64_t)blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
-  const int sp = (int)(lin % split);
-  const int64_t qt = (lin / split) * 4 + w;
+  const bool xcd_map = (split & 7) == 0;
+  const int sp = xcd_map ? (int)(lin % split) : (int)blockIdx.y;
+  const int64_t qt = (xcd_map ? lin / split : (int64_t)blockIdx.x) * 4 + w;
   if (qt * 32 >= nq) return;  // wave-uniform
   const int h = l >> 5;
   const int64_t q = qt * 32 + (l & 31);
