@@ -1,65 +1,167 @@
-"""MEPOL epoch benchmark on MI355X (BASELINE.json metric: epoch wall-clock + k-NN GB/s).
+"""MEPOL epoch benchmark on MI355X (BASELINE.json metric: epoch wall-clock + k-NN roofline).
 
-Workload (BASELINE configs[2], "C3"): Ant-shaped particle batch, N = 400 trajectories x 500
-steps = 200,000 particles, k-NN space d = 29 (full state), k = 30, policy 29 -> [400, 300] -> 8
-(f64, as the reference), Adam lr 1e-5, KL threshold 15, 30 off-policy iterations.  MuJoCo is
-out of scope, so the rollout phase is replaced by a seeded synthetic batch resident in HBM
-(states ~ N(0,1) f32, actions ~ N(0, 0.5^2) f32) -- the same on the CPU baseline leg.
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2|C2S|C3|C4|C5]
 
-One "step" = one MEPOL epoch inside the reference's timed window (mepol.py:405 -> 499) minus
-the rollout: exact k-NN over the next states + the off-policy loop (policy_update +
-compute_kl until the stop rule) + the final entropy.
+Workloads (BASELINE.json configs):
+  C3  (default) Ant-shaped batch: N = 400 x 500 = 200,000 particles, k-NN space d = 29, k = 30,
+      policy 29 -> [400, 300] -> 8 (f64, as the reference), Adam lr 1e-5, KL threshold 15,
+      30 off-policy iterations.  MuJoCo is out of scope, so the rollout is replaced by a seeded
+      synthetic batch resident in HBM (states ~ N(0,1) f32, actions ~ N(0, 0.5^2) f32); one
+      step = one epoch of the reference's timed window (mepol.py:405 -> 499) minus the rollout:
+      exact k-NN + off-policy loop (policy_update + compute_kl until the stop rule) + final H.
+  C4  Humanoid-shaped: N = 200,000, d = 47, k = 30, policy 47 -> [400, 300] -> 17.
+  C5  HandReach-shaped: N = 10,000 x 50 = 500,000, d = 63, k = 50, policy 63 -> [400, 300] -> 20.
+  C2  GridWorld, the whole epoch window including the rollout on the GPU: 20 x 1000 = 20,000
+      particles, k = 4 (BASELINE config), policy 2 -> [300, 300] -> 2, log_std -1.5.
+  C2S GridWorld at the reference script's settings (scripts/tae/grid_world.sh): 20 x 1200 =
+      24,000 particles, k = 50 -- the configuration SURVEY §6 timed at 9.10 s per epoch.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-Multi-GPU (one process per GPU, launched by torch.distributed.run): each rank owns
-N/world trajectories; next-states are all-gathered over RCCL before the k-NN, each rank answers
-its own queries, and the per-iteration scalars / weight vectors / parameter gradients are
-reduced so every rank takes the same steps (strong scaling: fixed N = 200k).
+Multi-GPU: one process per GPU.  Under torch.distributed.run (WORLD_SIZE set) each process is a
+rank; `--gpus N` without a launcher spawns the N ranks itself (fresh child processes, before
+any GPU call in the parent).  Rank r owns trajectories [r nt/N, (r+1) nt/N); next states are
+all-gathered (RCCL over xGMI) before the k-NN, each rank answers its own queries, and the
+per-iteration scalars / weight vectors / parameter gradients are reduced so every rank takes the
+same steps (strong scaling: fixed N).  With fewer GPUs than ranks the ranks share the GPUs over
+gloo and the line says "rehearsal".
 """
 import argparse
 import json
 import os
 import platform
+import socket
+import subprocess
+import sys
 import time
 
 import numpy as np
-import torch
 
-CFG = dict(num_traj=400, traj_len=500, nf=29, a=8, hidden=[400, 300], k=30, d=29, lr=1e-5,
-           kl_threshold=15.0, max_off_iters=30, backtrack_coeff=2, max_backtrack_try=10, eps=0.0)
+COMMON = dict(max_off_iters=30, backtrack_coeff=2, max_backtrack_try=10, lr=1e-5,
+              kl_threshold=15.0, eps=0.0, log_std_init=-0.5)
+WORKLOADS = {
+    "C3": dict(COMMON, num_traj=400, traj_len=500, nf=29, a=8, hidden=[400, 300], k=30, d=29,
+               name="C3 Ant-shaped MEPOL epoch (k-NN + off-policy loop + final H)"),
+    "C4": dict(COMMON, num_traj=400, traj_len=500, nf=47, a=17, hidden=[400, 300], k=30, d=47,
+               name="C4 Humanoid-shaped MEPOL epoch (k-NN + off-policy loop + final H)"),
+    "C5": dict(COMMON, num_traj=10000, traj_len=50, nf=63, a=20, hidden=[400, 300], k=50, d=63,
+               name="C5 HandReach-shaped MEPOL epoch (k-NN + off-policy loop + final H)"),
+    "C2": dict(COMMON, num_traj=20, traj_len=1000, nf=2, a=2, hidden=[300, 300], k=4, d=2,
+               log_std_init=-1.5, env="GridWorld",
+               name="C2 GridWorld MEPOL epoch (GPU rollout + k-NN + off-policy loop + final H)"),
+    "C2S": dict(COMMON, num_traj=20, traj_len=1200, nf=2, a=2, hidden=[300, 300], k=50, d=2,
+                log_std_init=-1.5, env="GridWorld",
+                name="C2S GridWorld MEPOL epoch at scripts/tae/grid_world.sh settings "
+                     "(GPU rollout + k-NN + off-policy loop + final H)"),
+}
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md: FP32 vector == FP32 matrix peak
 PEAK_F16_TFLOPS = 2500.0   # MI355X_MICROARCH.md: BF16/F16 MFMA ~2.5 PF dense
 PEAK_HBM_GBPS = 8000.0
+ROOT = os.path.dirname(os.path.abspath(__file__))
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-queries", type=int, default=16000)
-    return p.parse_args()
+    p.add_argument("--selftest", action="store_true",
+                   help="launcher plumbing only (no GPU): ranks rendezvous over gloo, time an "
+                        "empty step with the max-over-ranks clock and print the JSON line")
+    return p.parse_args(argv)
 
 
-def synthetic_batch(seed, device, rank=0, world=1):
+# ---------------------------------------------------------------------------------------------
+# launcher: --gpus N without torch.distributed.run
+# ---------------------------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn(args, argv):
+    """Start args.gpus rank processes (this file, same flags) and wait for them.  Runs before
+    any GPU call in this process (device_count does not initialise the GPU on this image)."""
+    import torch
+
+    n = args.gpus
+    ndev = torch.cuda.device_count()
+    backend = "nccl" if ndev >= n and not args.selftest else "gloo"
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   MEPOL_BENCH_BACKEND=backend, MEPOL_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
+# ---------------------------------------------------------------------------------------------
+# the benchmark proper (one rank)
+# ---------------------------------------------------------------------------------------------
+def synthetic_batch(cfg, seed, device, rank=0, world=1):
+    import torch
+
     g = torch.Generator(device=device).manual_seed(seed)
-    nt, T, nf, a = CFG["num_traj"], CFG["traj_len"], CFG["nf"], CFG["a"]
+    nt, T, nf, a = cfg["num_traj"], cfg["traj_len"], cfg["nf"], cfg["a"]
+    per = nt // world
     states = torch.randn((nt, T + 1, nf), generator=g, device=device, dtype=torch.float32)
     actions = 0.5 * torch.randn((nt, T, a), generator=g, device=device, dtype=torch.float32)
-    per = nt // world
-    return states[rank * per:(rank + 1) * per].contiguous(), actions[rank * per:(rank + 1) * per].contiguous()
+    return (states[rank * per:(rank + 1) * per].contiguous(),
+            actions[rank * per:(rank + 1) * per].contiguous())
 
 
-def main():
-    args = parse()
+def selftest(args):
+    """The multi-rank launch path without a GPU: rendezvous, barrier, max-over-ranks timing."""
+    import torch
+    import torch.distributed as dist
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    local = local % max(torch.cuda.device_count(), 1)
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    x = torch.full((1,), float(rank + 1), dtype=torch.float64)
+    for _ in range(args.steps):
+        if world > 1:
+            dist.all_reduce(x)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        dist.barrier()
+    if rank == 0:
+        print(json.dumps({"metric": "bench launcher selftest", "value": elapsed, "unit": "s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "selftest": True, "sum_of_ranks": float(x.item())}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run(args):
+    import torch
+
+    if args.selftest:
+        return selftest(args)
+    cfg = WORKLOADS[args.workload]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    ndev = max(torch.cuda.device_count(), 1)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % ndev
+    if world > 1 and args.gpus != world and rank == 0:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE",
+              file=sys.stderr)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
+    backend = None
     # MEPOL_BENCH_SHARDED=1 runs the multi-rank code path (ShardedEpoch + captured RCCL
     # collectives) at world size 1: a one-GPU rehearsal of what --gpus N runs per rank.
     sharded = world > 1 or os.environ.get("MEPOL_BENCH_SHARDED") == "1"
@@ -67,79 +169,97 @@ def main():
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29561")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
-
         backend = os.environ.get("MEPOL_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
-        else:  # rehearsal of the multi-rank path with several ranks on one GPU
+        else:  # rehearsal: several ranks share one GPU over gloo
             dist.init_process_group(backend)
     import scipy.special
 
-    from mepol_amd import ops
     from mepol_amd.algorithms import mepol as M
     from mepol_amd.policy import GaussianPolicy
 
-    k, nf, a, d = CFG["k"], CFG["nf"], CFG["a"], CFG["d"]
+    k, nf, a, d = cfg["k"], cfg["nf"], cfg["a"], cfg["d"]
+    nt, T = cfg["num_traj"], cfg["traj_len"]
+    if nt % world:
+        raise SystemExit(f"bench: {nt} trajectories do not split over {world} ranks")
     ns = d
     B = float(np.log(k) - scipy.special.digamma(k))
     G = float(scipy.special.gamma(ns / 2 + 1))
+    rollout = cfg.get("env") is not None
     torch.manual_seed(0)
-    behavioral = GaussianPolicy(CFG["hidden"], nf, a, -0.5).to(dev)
-    target = GaussianPolicy(CFG["hidden"], nf, a, -0.5).to(dev)
-    last_valid = GaussianPolicy(CFG["hidden"], nf, a, -0.5).to(dev)
+    env = None
+    if rollout:
+        from mepol_amd.envs import ErgodicEnv, GridWorldContinuous
+        from mepol_amd.policy import train_supervised
+
+        env = ErgodicEnv(GridWorldContinuous())
+        behavioral = GaussianPolicy(cfg["hidden"], nf, a, cfg["log_std_init"]).to(dev)
+        train_supervised(env, behavioral, 100, 5000)  # --zero_mean_start 1 (outside the window)
+        torch.cuda.manual_seed(1000 + rank)  # independent rollout noise / resets per rank
+    else:
+        behavioral = GaussianPolicy(cfg["hidden"], nf, a, cfg["log_std_init"]).to(dev)
+    target = GaussianPolicy(cfg["hidden"], nf, a, cfg["log_std_init"]).to(dev)
+    last_valid = GaussianPolicy(cfg["hidden"], nf, a, cfg["log_std_init"]).to(dev)
     target.load_state_dict(behavioral.state_dict())
     last_valid.load_state_dict(behavioral.state_dict())
-    opt = torch.optim.Adam(target.parameters(), lr=CFG["lr"])
-    N = CFG["num_traj"] * CFG["traj_len"]
+    opt = torch.optim.Adam(target.parameters(), lr=cfg["lr"])
+    N = nt * T
 
-    batches = [synthetic_batch(s, dev, rank, world) for s in range(3)]
-    knn_events = []
-    iters_done = []
+    batches = [] if rollout else [synthetic_batch(cfg, s, dev, rank, world) for s in range(3)]
+    knn_events, roll_events, iters_done, entropies = [], [], [], []
 
     def one_epoch(i):
-        states32, actions32 = batches[i % len(batches)]
-        nt_local = states32.shape[0]
-        T = CFG["traj_len"]
-        st = states32.double()
-        ac = actions32.double()
-        rtl = torch.full((nt_local, 1), T, dtype=torch.int64, device=dev)
-        nxt = states32[:, 1:].reshape(-1, nf)[:, :d].contiguous()
+        T_ = T
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
+        e2 = torch.cuda.Event(enable_timing=True)
         last_valid.load_state_dict(behavioral.state_dict())
+        e0.record()
+        if rollout:
+            st32, ac32, rtl32, nxt = M.collect_particles_device(env, behavioral, nt // world, T_,
+                                                                None)
+            nt_local = nt // world
+        else:
+            st32, ac32 = batches[i % len(batches)]
+            nt_local = st32.shape[0]
+            nxt = st32[:, 1:].reshape(-1, nf)[:, :d].contiguous()
+        e1.record()
+        st = st32.double()
+        ac = ac32.double()
+        rtl = torch.full((nt_local, 1), T_, dtype=torch.int64, device=dev)
         if not sharded:
-            e0.record()
             st_, ac_, rl_, _, D, I = M.make_particle_batch(st, ac, rtl, nxt, k)
-            e1.record()
+            e2.record()
             res = M.off_policy_optimization(
                 opt, behavioral, target, last_valid, st_, ac_, nt_local, rl_, D, I, k, G, B, ns,
-                CFG["eps"], CFG["kl_threshold"], CFG["max_off_iters"], True,
-                CFG["backtrack_coeff"], CFG["max_backtrack_try"], CFG["lr"])
+                cfg["eps"], cfg["kl_threshold"], cfg["max_off_iters"], True,
+                cfg["backtrack_coeff"], cfg["max_backtrack_try"], cfg["lr"])
         else:
             from mepol_amd.parallel import ShardedEpoch
 
             ep = ShardedEpoch(st, ac, rtl, nxt, k, dist)
-            e0.record()
             ep.build_knn()
-            e1.record()
+            e2.record()
             res = ep.off_policy_optimization(
-                opt, behavioral, target, last_valid, G, B, ns, CFG["eps"], CFG["kl_threshold"],
-                CFG["max_off_iters"], True, CFG["backtrack_coeff"], CFG["max_backtrack_try"],
-                CFG["lr"])
+                opt, behavioral, target, last_valid, G, B, ns, cfg["eps"], cfg["kl_threshold"],
+                cfg["max_off_iters"], True, cfg["backtrack_coeff"], cfg["max_backtrack_try"],
+                cfg["lr"])
         entropy, n_off, _, _ = res
         behavioral.load_state_dict(last_valid.state_dict())
         target.load_state_dict(last_valid.state_dict())
-        _ = float(entropy)
-        knn_events.append((e0, e1))
+        entropies.append(float(entropy))
+        roll_events.append((e0, e1))
+        knn_events.append((e1, e2))
         iters_done.append(n_off)
 
     for i in range(args.warmup):
         one_epoch(i)
-    knn_events.clear()
-    iters_done.clear()
+    for lst in (knn_events, roll_events, iters_done, entropies):
+        lst.clear()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -150,12 +270,18 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    knn_ms = float(np.mean([x.elapsed_time(y) for x, y in knn_events]))
+    roll_ms = float(np.mean([x.elapsed_time(y) for x, y in roll_events]))
+    per_rank_knn = [knn_ms]
     if dist is not None:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        kt = torch.tensor([knn_ms], device=dev, dtype=torch.float64)
+        allk = [torch.zeros_like(kt) for _ in range(world)]
+        dist.all_gather(allk, kt)
+        per_rank_knn = [float(x.item()) for x in allk]
     epoch_s = elapsed / args.steps
-    knn_ms = float(np.mean([a.elapsed_time(b) for a, b in knn_events]))
 
     if rank != 0:
         if dist is not None:
@@ -169,7 +295,6 @@ def main():
     iteration_path = "hip-graph replay" if it is not None and it.graph is not None else "eager"
     nq = N // world
     F = 3.0 * d * nq * N                      # algorithmic flops
-    B_scan = 4.0 * d * nq * N                 # algorithmic scan bytes
     knn_tflops = F / (knn_ms * 1e-3) / 1e12
     # Which selection the library ran (include/mepol_amd.h; MEPOL_KNN_PRECISION=f32 forces f32):
     # split-f16 issues 3 products x 2 x K flops per (query, candidate), K = 16*ceil((d+1)/16).
@@ -182,16 +307,19 @@ def main():
         knn_issued = 2 * 2 * ((d + 2) // 2) * float(nq) * N
         knn_peak = PEAK_FP32_TFLOPS
         knn_desc = "fp32 MFMA selection + f64 exact refine (bit-exact output)"
-    knn_gbps = B_scan / (knn_ms * 1e-3) / 1e9
     traffic = None
-    pmc_path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "knn_pmc.json")
+    pmc_path = os.path.join(ROOT, "profiles", f"knn_pmc_{args.workload}.json")
+    if args.workload == "C3" and not os.path.exists(pmc_path):
+        pmc_path = os.path.join(ROOT, "profiles", "knn_pmc.json")
     if os.path.exists(pmc_path) and world == 1:  # counters were taken on the 1-GPU k-NN call
         try:
             traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    rehearsal = sharded and backend != "nccl" and world > 1
     line = {
-        "metric": "MEPOL epoch wall-clock (C3 Ant-shaped, N=200k, d=29, k=30; rollout excluded)",
+        "metric": f"MEPOL epoch wall-clock ({args.workload}: N={N}, d={d}, k={k}"
+                  + ("; rollout included)" if rollout else "; rollout excluded)"),
         "value": round(epoch_s, 6),
         "unit": "s/epoch",
         "n_gpus": world,
@@ -202,66 +330,113 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic",
-        "config": {"workload": "C3 Ant-shaped MEPOL epoch (k-NN + off-policy loop + final H)",
-                   "particles": N, "num_traj": CFG["num_traj"], "traj_len": CFG["traj_len"],
-                   "d": d, "k": k, "policy": f"{nf}->{CFG['hidden']}->{a} f64",
+        "data": "synthetic" if not rollout else "GridWorld rollouts of a random-init policy",
+        "config": {"workload": cfg["name"], "particles": N, "num_traj": nt, "traj_len": T,
+                   "d": d, "k": k, "policy": f"{nf}->{cfg['hidden']}->{a} f64",
                    "off_policy_iters": float(np.mean(iters_done)), "parallelism": f"dp{world}",
-                   "knn_precision": knn_desc,
-                   "off_policy_iteration": iteration_path},
+                   "knn_precision": knn_desc, "off_policy_iteration": iteration_path},
         "particles_per_s": round(N / epoch_s, 1),
         "knn_ms": round(knn_ms, 3),
-        "knn_scan_GBps": round(knn_gbps, 1),
-        "knn_scan_frac_of_8TBps": round(knn_gbps / PEAK_HBM_GBPS, 3),
+        "knn_ms_per_rank": [round(x, 3) for x in per_rank_knn],
         "roofline": {"bound": "mfma", "achieved": round(knn_tflops, 2), "peak": knn_peak,
                      "unit": "TFLOP/s", "frac": round(knn_tflops / knn_peak, 4),
                      "mfma_issued_tflops": round(knn_issued / (knn_ms * 1e-3) / 1e12, 2),
                      "traffic": traffic,
-                     "kernel": "k-NN (norms+pack+select+refine+exact), achieved = F/t with F = 3*d*Nq*Nc (SURVEY 8d); the select is VALU-issue-bound (threshold/merge work), not MFMA-bound"},
+                     "kernel": "k-NN call (norms + pack + select + refine + exact), HIP events on "
+                               "the launch stream; achieved = F/t, F = 3*d*Nq*Nc (SURVEY 8d)"},
     }
+    if traffic:
+        gbps = traffic / (knn_ms * 1e-3) / 1e9
+        line["roofline"]["hbm_GBps"] = round(gbps, 1)
+        line["roofline"]["hbm_frac"] = round(gbps / PEAK_HBM_GBPS, 4)
+    if rollout:
+        line["rollout_ms"] = round(roll_ms, 3)
+        line["rollout_us_per_step"] = round(roll_ms * 1e3 / T, 2)
+        line["final_entropy"] = float(np.mean(entropies))
+        line["survey_reference_epoch_s"] = 9.10 if args.workload == "C2S" else None
+    if rehearsal:
+        line["config"]["rehearsal"] = f"{world} ranks on {torch.cuda.device_count()} GPU(s), gloo"
     if not args.no_cpu_baseline and world == 1:
-        line["cpu_baseline"] = cpu_baseline(args.cpu_sample_queries)
+        line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample_queries, iters_done)
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
-def cpu_baseline(sample_queries):
-    """The oracle (reference-shaped CPU restatement, torch f64 + sklearn) on host cores.
+# ---------------------------------------------------------------------------------------------
+# CPU baseline: the oracle (reference-shaped CPU restatement) on the host cores
+# ---------------------------------------------------------------------------------------------
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or platform.machine()
 
-    Bounded sample: sklearn k-NN for `sample_queries` queries against all 200k candidates
-    (scaled by 200k / sample_queries), one policy_update + one compute_kl at full N
-    (scaled by the GPU run's iteration count), plus one final-entropy forward."""
+
+def _cpu_threads():
+    """Host threads for the baseline: the CPUs this process may run on, capped by the box's
+    declared share (OMP_NUM_THREADS is set to it on the GPU box)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return (min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff), aff
+
+
+def cpu_baseline(cfg, sample_queries, iters_done):
+    """Bounded sample of one epoch on the oracle (torch f64 + sklearn, reference-shaped):
+    sklearn k-NN for `sample_queries` queries against all candidates (scaled to N queries), one
+    policy_update + one compute_kl at full N (scaled by the GPU run's iteration count) plus the
+    final entropy, and for rollout workloads the reference's per-step batch-1 rollout over two
+    trajectories (scaled to num_traj)."""
+    import torch
+    import scipy.special
     import sklearn
     from sklearn.neighbors import NearestNeighbors
 
     from oracle import mepol_oracle as O
 
-    cores = min(16, len(os.sched_getaffinity(0)))
+    cores, aff = _cpu_threads()
     torch.set_num_threads(cores)
-    k, nf, a, d = CFG["k"], CFG["nf"], CFG["a"], CFG["d"]
-    nt, T = CFG["num_traj"], CFG["traj_len"]
+    k, nf, a, d = cfg["k"], cfg["nf"], cfg["a"], cfg["d"]
+    nt, T = cfg["num_traj"], cfg["traj_len"]
+    N = nt * T
     rng = np.random.default_rng(0)
-    X = rng.standard_normal((nt * T, d)).astype(np.float32)
+    torch.manual_seed(0)
+    beh = O.TorchPolicy(cfg["hidden"], nf, a, cfg["log_std_init"])
+    tgt = O.TorchPolicy(cfg["hidden"], nf, a, cfg["log_std_init"])
+    tgt.load_state_dict(beh.state_dict())
+    roll_s = 0.0
+    if cfg.get("env") == "GridWorld":
+        # collect_particles (mepol.py:76-109): batch-1 policy.predict + env.step per step
+        nsamp = 2
+        t = time.perf_counter()
+        std = torch.exp(beh.log_std.detach())
+        for _ in range(nsamp):
+            s = rng.uniform(-6, -4, (1, 2)).astype(np.float32)
+            for _t in range(T):
+                with torch.no_grad():
+                    mu = beh.mean(beh.net(torch.as_tensor(s, dtype=torch.float64)))
+                    act = (mu + torch.randn(mu.shape, dtype=torch.float64) * std).numpy()
+                s = O.gridworld_step(s, act)
+        roll_s = (time.perf_counter() - t) * nt / nsamp
+        X = rng.uniform(-6, 6, (N, d)).astype(np.float32)
+    else:
+        X = rng.standard_normal((N, d)).astype(np.float32)
+    nq = min(sample_queries, N)
     t = time.perf_counter()
     nbrs = NearestNeighbors(n_neighbors=k + 1, metric="euclidean", algorithm="auto", n_jobs=cores)
     nbrs.fit(X)
-    Dq, Iq = nbrs.kneighbors(X[:sample_queries])
-    knn_s = (time.perf_counter() - t) * (X.shape[0] / sample_queries)
-    # full-N iteration on reference-shaped torch CPU code (per-trajectory loops)
-    torch.manual_seed(0)
-    beh = O.TorchPolicy(CFG["hidden"], nf, a)
-    tgt = O.TorchPolicy(CFG["hidden"], nf, a)
-    tgt.load_state_dict(beh.state_dict())
-    opt = torch.optim.Adam(tgt.parameters(), lr=CFG["lr"])
+    nbrs.kneighbors(X[:nq])
+    knn_s = (time.perf_counter() - t) * (N / nq)
+    opt = torch.optim.Adam(tgt.parameters(), lr=cfg["lr"])
     S = torch.as_tensor(rng.standard_normal((nt, T + 1, nf)), dtype=torch.float64)
     A = torch.as_tensor(0.5 * rng.standard_normal((nt, T, a)), dtype=torch.float64)
     lengths = [T] * nt
     # neighbour table of the right shape (values irrelevant to the timing)
-    I = torch.as_tensor(rng.integers(0, nt * T, (nt * T, k + 1)), dtype=torch.int64)
-    D = torch.as_tensor(rng.random((nt * T, k + 1)) + 1.0, dtype=torch.float64)
-    import scipy.special
-
+    I = torch.as_tensor(rng.integers(0, N, (N, k + 1)), dtype=torch.int64)
+    D = torch.as_tensor(rng.random((N, k + 1)) + 1.0, dtype=torch.float64)
     B = float(np.log(k) - scipy.special.digamma(k))
     G = float(scipy.special.gamma(d / 2 + 1))
     t = time.perf_counter()
@@ -271,14 +446,27 @@ def cpu_baseline(sample_queries):
     with torch.no_grad():
         O.torch_kl(beh, tgt, S, A, nt, lengths, I, k, 0.0)
     kl_s = time.perf_counter() - t
-    epoch_s = knn_s + CFG["max_off_iters"] * (upd_s + kl_s) + kl_s
+    iters = float(np.mean(iters_done)) if iters_done else float(cfg["max_off_iters"])
+    epoch_s = roll_s + knn_s + iters * (upd_s + kl_s) + kl_s
+    sample = (f"sklearn {sklearn.__version__} NearestNeighbors(auto, n_jobs={cores}) on {nq} of "
+              f"{N} queries x {N} candidates (scaled x{N / nq:.1f}) = {knn_s:.2f} s; one "
+              f"policy_update {upd_s:.2f} s + compute_kl {kl_s:.2f} s at full N "
+              f"(x{iters:g} + final H)")
+    if roll_s:
+        sample += f"; batch-1 rollout of 2 of {nt} trajectories x {T} steps (scaled) = {roll_s:.2f} s"
     return {"value": round(epoch_s, 3), "unit": "s/epoch", "cores": cores, "kind": "port",
-            "sample": (f"sklearn {sklearn.__version__} NearestNeighbors(auto, n_jobs={cores}) on "
-                       f"{sample_queries} of 200000 queries x 200000 candidates (scaled x"
-                       f"{X.shape[0] / sample_queries:.1f}) = {knn_s:.2f} s; one policy_update "
-                       f"{upd_s:.2f} s + compute_kl {kl_s:.2f} s at full N (x30 + final H); "
-                       f"torch f64 CPU, {platform.processor() or platform.machine()}")}
+            "sample": sample + "; torch f64 CPU", "cpu_model": _cpu_model(),
+            "affinity_cpus": aff}
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn(args, argv)
+    run(args)
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

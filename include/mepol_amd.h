@@ -44,7 +44,11 @@ int mepol_abi_version(void);
  * arithmetic), rows ascending, ties by smaller index; idx_out [n_query, kp1] int64 (nullable);
  * idx32_out [kp1, n_query] int32 TRANSPOSED (nullable; the layout the entropy kernels read).
  * n_fallback_out (nullable, device int32): number of queries answered by the exhaustive path.
- * split_hint: 0 = automatic candidate split.  Fast path: d <= 63, kp1 <= 60. */
+ * split_hint: 0 = automatic candidate split.  Fast path: d <= 63, kp1 <= 60.
+ * Input validation (sklearn's check_array in fit/kneighbors): a NaN / inf coordinate in cand or
+ * query returns MEPOL_ERR_BAD_ARG ("Input contains NaN or infinity"); a row whose f32 squared
+ * norm overflows returns MEPOL_ERR_UNSUPPORTED.  The check synchronises `stream` once per call
+ * (before the scan is launched), as the reference's kneighbors call blocks. */
 int mepol_knn_workspace_size(int64_t n_cand, int64_t n_query, int d, int kp1, int split_hint,
                              size_t* bytes);
 int mepol_knn_plan_info(int64_t n_cand, int64_t n_query, int d, int kp1, int split_hint, int* ks,

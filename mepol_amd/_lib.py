@@ -64,6 +64,11 @@ class MepolError(RuntimeError):
     pass
 
 
+class MepolInputError(MepolError, ValueError):
+    """MEPOL_ERR_BAD_ARG: invalid input (e.g. non-finite particles); a ValueError like the
+    reference's sklearn check_array rejection."""
+
+
 def load():
     """Load libmepol_amd.so (once) and bind every exported symbol; raise if unavailable."""
     global _lib
@@ -90,7 +95,8 @@ def call(name, *args):
     rc = getattr(lib, name)(*args)
     if rc != 0:
         msg = lib.mepol_last_error_string()
-        raise MepolError(f"{name} failed (rc={rc}): {msg.decode() if msg else ''}")
+        cls = MepolInputError if rc == 1001 else MepolError
+        raise cls(f"{name} failed (rc={rc}): {msg.decode() if msg else ''}")
     return rc
 
 

@@ -118,6 +118,10 @@ class DeviceIteration:
         self.scal = torch.zeros(8, **f64)
         self.scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
         self.vals = torch.zeros(2, **f64)
+        # scratch owned by this graph (never the eager per-stream cache, whose buffers can be
+        # replaced while a captured graph still holds their addresses)
+        self.ws_head = ops.head_workspace(self.N, W2.shape[0], Wm.shape[0], dev)
+        self.ws_layer = ops.layer_workspace(self.N, W1.shape[1], W1.shape[0], dev)
         self.graph = None
         self.fork = torch.cuda.Stream(device=dev)
         self._batch_id = None
@@ -216,7 +220,7 @@ class DeviceIteration:
                                         self.neg_one)
         # through the policy (the _TwoLayerLogp backward)
         dz2, dWm, dbm, dls, db2 = ops.head_backward(grad.view(-1), self.z2, Wm, ls, self.act,
-                                                    self.mu, bz=b2, need_dz=True)
+                                                    self.mu, bz=b2, need_dz=True, ws=self.ws_head)
         # dW2 (split-K GEMM) on a forked stream, concurrent with dh1 -> layer-1 backward: the
         # memory-bound layer kernel overlaps the MFMA-bound GEMM.
         cur = torch.cuda.current_stream()
@@ -224,7 +228,7 @@ class DeviceIteration:
         with torch.cuda.stream(self.fork):
             dW2 = _weight_grad(dz2, self.h1)
         dh1 = torch.mm(dz2, W2)
-        dW1, db1 = ops.layer_backward(dh1, self.h1, self.x)
+        dW1, db1 = ops.layer_backward(dh1, self.h1, self.x, ws=self.ws_layer)
         cur.wait_stream(self.fork)
         # optimizer.step() (mepol.py:280)
         grad_of = {id(p): g for p, g in zip(self.named, (dW1, db1, dW2, db2, dWm, dbm, dls))}

@@ -42,7 +42,7 @@ def _batched_kind(env):
 
 
 def collect_particles_device(env, policy, num_traj, traj_len, state_filter, generator=None,
-                             visited=None):
+                             visited=None, shard=None):
     """Rollout of num_traj trajectories of traj_len steps, batched on the policy's device.
 
     Returns device tensors: states f32 [nt, T+1, nf], actions f32 [nt, T, a], real lengths
@@ -51,6 +51,12 @@ def collect_particles_device(env, policy, num_traj, traj_len, state_filter, gene
     any other env is stepped on the host in lockstep with one batched policy call per step.
     `visited` (optional, f64 [nt, T, nf]) receives the env's own state after every step (f64
     MountainCar state / GridWorld f32 state, not the f32 particle copy), for the heatmap.
+
+    shard=(rank, world): roll out only trajectories [rank nt/world, (rank+1) nt/world) of the
+    num_traj-trajectory batch.  The initial states and the action noise of ALL trajectories are
+    drawn up front ([T, nt, a] f64, one draw), so a trajectory's randomness does not depend on
+    how the batch is split: the shards of `world` ranks concatenate to the one-rank rollout (the
+    reference's loky workers instead start from copies of one RNG state).
     """
     dev = policy.device
     if dev.type != "cuda":
@@ -60,12 +66,20 @@ def collect_particles_device(env, policy, num_traj, traj_len, state_filter, gene
     nf = env.num_features
     a_dim = env.action_space.shape[0]
     T = int(traj_len)
+    rank, world = shard if shard is not None else (0, 1)
+    if num_traj % world:
+        raise ValueError(f"{num_traj} trajectories do not split over {world} ranks")
+    total = num_traj
+    num_traj = total // world
+    lo, hi = rank * num_traj, (rank + 1) * num_traj
     states = torch.zeros((num_traj, T + 1, nf), dtype=torch.float32, device=dev)
     actions = torch.zeros((num_traj, T, a_dim), dtype=torch.float32, device=dev)
     with torch.no_grad():
         if kind in ("mountaincar", "gridworld"):
             env_id = 0 if kind == "mountaincar" else 1
-            init = base.reset_batch_torch(num_traj, dev, generator)
+            init = base.reset_batch_torch(total, dev, generator)[lo:hi]
+            noise_all = torch.randn((T, total, a_dim), dtype=torch.float64, device=dev,
+                                    generator=generator)
             env64 = init.clone() if env_id == 0 else None
             env32 = init.clone() if env_id == 1 else None
             policy_in = init.to(torch.float64).contiguous()
@@ -73,13 +87,14 @@ def collect_particles_device(env, policy, num_traj, traj_len, state_filter, gene
             log_std = policy.log_std.detach().contiguous()
             for t in range(T):
                 mean = policy.mean_action(policy_in).contiguous()
-                noise = torch.randn(mean.shape, dtype=torch.float64, device=dev,
-                                    generator=generator)
+                noise = noise_all[t, lo:hi]
                 ops.rollout_step(env_id, env64, env32, mean, noise, log_std, t, T, states, actions,
                                  policy_in)
                 if visited is not None:
                     visited[:, t].copy_(policy_in)
         else:
+            if world > 1:
+                raise NotImplementedError("sharded rollouts need a batched (HIP-stepped) env")
             envs = [env] + [_clone_env(env) for _ in range(num_traj - 1)]
             s = np.stack([e.reset() for e in envs])
             states[:, 0] = torch.as_tensor(s, dtype=torch.float32, device=dev)
@@ -339,6 +354,8 @@ def policy_update(optimizer, behavioral_policy, target_policy, states, actions, 
 # ---------------------------------------------------------------------------------------------
 def _summary_writer(out_path):
     try:
+        if out_path is None:  # non-zero ranks of a multi-rank run log nothing
+            raise RuntimeError
         from torch.utils import tensorboard  # noqa: F401
 
         return tensorboard.SummaryWriter(out_path)
@@ -351,6 +368,22 @@ def _summary_writer(out_path):
                 pass
 
         return _Null()
+
+
+def _distributed():
+    """torch.distributed when a multi-rank process group is up (mepol() then shards), else None."""
+    try:
+        import torch.distributed as dist
+    except ImportError:  # pragma: no cover
+        return None
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist
+    return None
+
+
+def _is_rank0():
+    d = _distributed()
+    return d is None or d.get_rank() == 0
 
 
 def log_epoch_statistics(writer, log_file, csv_file_1, csv_file_2, epoch, loss, entropy,
@@ -387,7 +420,8 @@ def log_epoch_statistics(writer, log_file, csv_file_1, csv_file_2, epoch, loss, 
         csv_file_2.flush()
     log_file.write(grid)
     log_file.flush()
-    print(grid)
+    if _is_rank0():
+        print(grid)
 
 
 def log_off_iter_statistics(writer, csv_file_3, epoch, global_off_iter, num_off_iter, entropy, kl,
@@ -414,7 +448,17 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
 
     Heatmaps (mepol.py:19-67) are computed on the device (get_heatmap) when a discretizer is
     given, at epoch 0 and every heatmap_every epochs, and logged to {env_name}-heatmap.csv.
+
+    Multi-rank (a torch.distributed group of world > 1 is initialised, one process per GPU):
+    the particle batch is sharded by trajectory -- the reference's worker split, mepol.py:179-187
+    -- and every rank holds the same policies, optimizer state and control decisions
+    (parallel.ShardedEpoch: RCCL all-gather of next states before the k-NN, fixed-order
+    reductions per iteration).  Rank 0 writes the logs, CSVs and checkpoints.
     """
+    dist = _distributed()
+    rank, world = (dist.get_rank(), dist.get_world_size()) if dist is not None else (0, 1)
+    if num_traj % world:
+        raise ValueError(f"num_traj={num_traj} does not split over {world} ranks")
     if seed is not None:
         np.random.seed(seed)
         torch.manual_seed(seed)
@@ -433,14 +477,18 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
     else:
         raise NotImplementedError
 
-    writer = _summary_writer(out_path)
-    log_file = open(os.path.join(out_path, "log_file.txt"), "a", encoding="utf-8")
-    csv_file_1 = open(os.path.join(out_path, f"{env_name}.csv"), "w")
+    def out(name, mode="w"):  # rank 0 writes the run's files; the other ranks discard
+        return open(os.path.join(out_path, name) if rank == 0 else os.devnull, mode,
+                    encoding="utf-8")
+
+    writer = _summary_writer(out_path) if rank == 0 else _summary_writer(None)
+    log_file = out("log_file.txt", "a")
+    csv_file_1 = out(f"{env_name}.csv")
     csv_file_1.write(",".join(["epoch", "loss", "entropy", "full_entropy", "num_off_iters",
                                "execution_time"]))
     csv_file_1.write("\n")
     if heatmap_discretizer is not None:
-        csv_file_2 = open(os.path.join(out_path, f"{env_name}-heatmap.csv"), "w")
+        csv_file_2 = out(f"{env_name}-heatmap.csv")
         csv_file_2.write(",".join(["epoch", "average_entropy"]))
         csv_file_2.write("\n")
     else:
@@ -453,7 +501,7 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
                                   heatmap_num_steps, heatmap_cmap, heatmap_interp, heatmap_labels)
         return h, image
 
-    csv_file_3 = open(os.path.join(out_path, f"{env_name}_off_policy_iter.csv"), "w")
+    csv_file_3 = out(f"{env_name}_off_policy_iter.csv")
     csv_file_3.write(",".join(["epoch", "off_policy_iter", "entropy", "kl", "learning_rate"]))
     csv_file_3.write("\n")
 
@@ -462,28 +510,44 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
     full_B = np.log(full_entropy_k) - scipy.special.digamma(full_entropy_k)
     G = scipy.special.gamma(ns / 2 + 1)
 
+    def collect(nt, kk):
+        """The epoch's particles: the reference's 6-tuple (one rank) or a ShardedEpoch."""
+        if dist is None:
+            return collect_particles_and_compute_knn(env, behavioral_policy, nt, traj_len,
+                                                     state_filter, kk, num_workers)
+        from ..parallel import ShardedEpoch
+
+        assert nt % num_workers == 0, "Please provide a number of trajectories " \
+                                      "that can be equally split among workers"
+        s32, a32, r32, ns32 = collect_particles_device(env, behavioral_policy, nt, traj_len,
+                                                       state_filter, shard=(rank, world))
+        ep = ShardedEpoch(s32.to(float_type), a32.to(float_type), r32.to(int_type), ns32, kk,
+                          dist)
+        ep.build_knn()
+        return ep
+
+    def no_grad_entropy(batch, nt, kk, BB):
+        with torch.no_grad():
+            if dist is not None:
+                return batch.compute_entropy(behavioral_policy, behavioral_policy, kk, G, BB, ns,
+                                             eps)
+            st, ac, rl, _, D, I = batch
+            return compute_entropy(behavioral_policy, behavioral_policy, st, ac, nt, rl, D, I, kk,
+                                   G, BB, ns, eps)
+
     epoch = 0
     _sync()
     t0 = time.time()
-    states, actions, real_traj_lengths, next_states, distances, indices = \
-        collect_particles_and_compute_knn(env, behavioral_policy, num_traj * full_entropy_traj_scale,
-                                          traj_len, state_filter, full_entropy_k, num_workers)
-    with torch.no_grad():
-        full_entropy = compute_entropy(behavioral_policy, behavioral_policy, states, actions,
-                                       num_traj * full_entropy_traj_scale, real_traj_lengths,
-                                       distances, indices, full_entropy_k, G, full_B, ns, eps)
-    states, actions, real_traj_lengths, next_states, distances, indices = \
-        collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len, state_filter,
-                                          k, num_workers)
-    with torch.no_grad():
-        entropy = compute_entropy(behavioral_policy, behavioral_policy, states, actions, num_traj,
-                                  real_traj_lengths, distances, indices, k, G, B, ns, eps)
+    full_entropy = no_grad_entropy(collect(num_traj * full_entropy_traj_scale, full_entropy_k),
+                                   num_traj * full_entropy_traj_scale, full_entropy_k, full_B)
+    entropy = no_grad_entropy(collect(num_traj, k), num_traj, k, B)
     full_entropy = _np(full_entropy)
     entropy = _np(entropy)
     execution_time = time.time() - t0
     loss = -entropy
     heatmap_entropy, heatmap_image = heatmap()
-    _save_policy(behavioral_policy, os.path.join(out_path, f"{epoch}-policy"))
+    if rank == 0:
+        _save_policy(behavioral_policy, os.path.join(out_path, f"{epoch}-policy"))
     log_epoch_statistics(writer=writer, log_file=log_file, csv_file_1=csv_file_1,
                          csv_file_2=csv_file_2, epoch=epoch, loss=loss, entropy=entropy,
                          execution_time=execution_time, num_off_iters=0, full_entropy=full_entropy,
@@ -498,9 +562,7 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
         t0 = time.time()
         last_valid_target_policy.load_state_dict(behavioral_policy.state_dict())
 
-        states, actions, real_traj_lengths, next_states, distances, indices = \
-            collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len,
-                                              state_filter, k, num_workers)
+        batch = collect(num_traj, k)
 
         def on_accept(num_off_iters, entropy, kl, lr):
             nonlocal global_num_off_iters
@@ -508,11 +570,19 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
             log_off_iter_statistics(writer, csv_file_3, epoch, global_num_off_iters,
                                     num_off_iters - 1, entropy, kl, lr)
 
-        res = off_policy_optimization(
-            optimizer, behavioral_policy, target_policy, last_valid_target_policy, states,
-            actions, num_traj, real_traj_lengths, distances, indices, k, G, B, ns, eps,
-            kl_threshold, max_off_iters, use_backtracking, backtrack_coeff, max_backtrack_try,
-            original_lr if use_backtracking else learning_rate, on_accept)
+        lr0 = original_lr if use_backtracking else learning_rate
+        if dist is not None:
+            res = batch.off_policy_optimization(
+                optimizer, behavioral_policy, target_policy, last_valid_target_policy, G, B, ns,
+                eps, kl_threshold, max_off_iters, use_backtracking, backtrack_coeff,
+                max_backtrack_try, lr0, on_accept)
+        else:
+            states, actions, real_traj_lengths, next_states, distances, indices = batch
+            res = off_policy_optimization(
+                optimizer, behavioral_policy, target_policy, last_valid_target_policy, states,
+                actions, num_traj, real_traj_lengths, distances, indices, k, G, B, ns, eps,
+                kl_threshold, max_off_iters, use_backtracking, backtrack_coeff, max_backtrack_try,
+                lr0, on_accept)
         entropy, num_off_iters, backtrack_iter, learning_rate = res
         if torch.isnan(entropy) or torch.isinf(entropy):
             print("Aborting because final entropy is nan or inf...")
@@ -528,17 +598,12 @@ def mepol(env, env_name, state_filter, create_policy, k, kl_threshold, max_off_i
         heatmap_entropy, heatmap_image = None, None
         if epoch % heatmap_every == 0:
             heatmap_entropy, heatmap_image = heatmap()
-            states, actions, real_traj_lengths, next_states, distances, indices = \
-                collect_particles_and_compute_knn(env, behavioral_policy,
-                                                  num_traj * full_entropy_traj_scale, traj_len,
-                                                  state_filter, full_entropy_k, num_workers)
-            with torch.no_grad():
-                full_entropy = compute_entropy(behavioral_policy, behavioral_policy, states,
-                                               actions, num_traj * full_entropy_traj_scale,
-                                               real_traj_lengths, distances, indices,
-                                               full_entropy_k, G, full_B, ns, eps)
+            full_entropy = no_grad_entropy(
+                collect(num_traj * full_entropy_traj_scale, full_entropy_k),
+                num_traj * full_entropy_traj_scale, full_entropy_k, full_B)
             full_entropy = _np(full_entropy)
-            _save_policy(behavioral_policy, os.path.join(out_path, f"{epoch}-policy"))
+            if rank == 0:
+                _save_policy(behavioral_policy, os.path.join(out_path, f"{epoch}-policy"))
         log_epoch_statistics(writer=writer, log_file=log_file, csv_file_1=csv_file_1,
                              csv_file_2=csv_file_2, epoch=epoch, loss=loss, entropy=entropy,
                              execution_time=execution_time, num_off_iters=num_off_iters,

@@ -23,7 +23,7 @@ namespace head {
 #define MEPOL_HEAD_BWD_PF 1  // rows prefetched per wave in head_bwd_kernel
 #endif
 
-constexpr int kMaxA = 8;      // fused path: action_dim <= 8 (MountainCar 1, GridWorld 2, Ant 8)
+constexpr int kMaxA = 32;     // fused path: action_dim <= 32 (MC 1, GW 2, Ant 8, Humanoid 17, HandReach 20)
 constexpr int kMaxCols = 8;   // columns per lane: hidden <= 512
 constexpr double kLog2Pi = 1.8378770664093453;
 constexpr double kStdEps = 1e-7;
@@ -69,29 +69,31 @@ __device__ __forceinline__ double reduce_scatter_g(double (&v)[AP], int l, int& 
 // form spent most of its time in the 64-lane reduction and its selects).  Wm, bz and the
 // per-component constants live in LDS; loads of z are 4 rows x 128 B segments, next group
 // prefetched.
-template <int AP, int NCL>
+template <int AP, int NCL, int NCH>
 __global__ __launch_bounds__(256) void head_fwd16_kernel(
     const double* __restrict__ z, int64_t N, int H, const double* __restrict__ bz,
     const double* __restrict__ Wm, const double* __restrict__ bm,
     const double* __restrict__ log_std, const double* __restrict__ act, int A,
     double* __restrict__ mu_out, double* __restrict__ logp_out) {
   constexpr int AP2 = AP >= 2 ? AP / 2 : 1;
-  __shared__ double2 sW2[NCL * AP2 * 16];  // [j][a/2][q] pairs (a even, a+1)
-  __shared__ double sB[NCL * 16];          // [j][q] folded bias of z
-  __shared__ double sK[3][AP];             // bm, log 2pi + 2 log_std, 1/sigma^2
+  constexpr int APT = AP * NCH;                // action slots (chunks of AP)
+  __shared__ double2 sW2[NCH * NCL * AP2 * 16];  // [chunk][j][a/2][q] pairs (a even, a+1)
+  __shared__ double sB[NCL * 16];                // [j][q] folded bias of z
+  __shared__ double sK[3][APT];                  // bm, log 2pi + 2 log_std, 1/sigma^2
   const int l = threadIdx.x & 63;
   const int q = l & 15, r = l >> 4;
-  for (int e = threadIdx.x; e < NCL * AP2 * 16; e += blockDim.x) {
-    const int qq = e & 15, a2 = (e >> 4) % AP2, j = (e >> 4) / AP2;
+  for (int e = threadIdx.x; e < NCH * NCL * AP2 * 16; e += blockDim.x) {
+    const int qq = e & 15, a2 = (e >> 4) % AP2, j = ((e >> 4) / AP2) % NCL;
+    const int ch = (e >> 4) / (AP2 * NCL);
     const int c = qq + 16 * j;
-    const int a0 = 2 * a2, a1 = 2 * a2 + 1;
+    const int a0 = ch * AP + 2 * a2, a1 = a0 + 1;
     double2 w;
     w.x = (c < H && a0 < A) ? Wm[a0 * H + c] : 0.0;
     w.y = (AP >= 2 && c < H && a1 < A) ? Wm[a1 * H + c] : 0.0;
     sW2[e] = w;
   }
   for (int e = threadIdx.x; e < NCL * 16; e += blockDim.x) sB[e] = (bz && e < H) ? bz[e] : 0.0;
-  if (threadIdx.x < AP) {
+  if (threadIdx.x < APT) {
     const int a = threadIdx.x;
     const double lsa = (a < A) ? log_std[a] : 0.0;
     const double sd = exp(lsa) + kStdEps;
@@ -122,31 +124,39 @@ __global__ __launch_bounds__(256) void head_fwd16_kernel(
     for (int j = 0; j < NCL; ++j) zc[j] = zn[j];
     load_group(gi + nwaves);
     const int64_t row = gi * 4 + r;
-    double acc[AP];
-#pragma unroll
-    for (int a = 0; a < AP; ++a) acc[a] = 0.0;
     int qo = q;
     asm volatile("" : "+v"(qo));  // keep the LDS reads inside the loop
+    if (NCH > 1) {  // relu(z + b) once, reused by every chunk
 #pragma unroll
-    for (int j = 0; j < NCL; ++j) {
-      const double x = fmax(zc[j] + sB[j * 16 + qo], 0.0);
-#pragma unroll
-      for (int a2 = 0; a2 < AP2; ++a2) {
-        const double2 w = sW2[(j * AP2 + a2) * 16 + qo];
-        acc[2 * a2] = fma(x, w.x, acc[2 * a2]);
-        if (AP >= 2) acc[2 * a2 + 1] = fma(x, w.y, acc[2 * a2 + 1]);
-      }
+      for (int j = 0; j < NCL; ++j) zc[j] = fmax(zc[j] + sB[j * 16 + qo], 0.0);
     }
-    int a;
-    const double v = reduce_scatter_g<AP, 16>(acc, l, a);
     // lanes of a row with equal component: (16 / AP) of them; the lowest one writes
     const bool writer = (q & ((16 / AP) - 1)) == 0;
     double term = 0.0;
-    if (row < N && a < A && writer) {
-      const double m = v + sK[0][a];
-      const double d = act[row * A + a] - m;
-      mu_out[row * A + a] = m;
-      term = -0.5 * (sK[1][a] + d * d * sK[2][a]);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      double acc[AP];
+#pragma unroll
+      for (int a = 0; a < AP; ++a) acc[a] = 0.0;
+#pragma unroll
+      for (int j = 0; j < NCL; ++j) {
+        const double x = NCH > 1 ? zc[j] : fmax(zc[j] + sB[j * 16 + qo], 0.0);
+#pragma unroll
+        for (int a2 = 0; a2 < AP2; ++a2) {
+          const double2 w = sW2[((ch * NCL + j) * AP2 + a2) * 16 + qo];
+          acc[2 * a2] = fma(x, w.x, acc[2 * a2]);
+          if (AP >= 2) acc[2 * a2 + 1] = fma(x, w.y, acc[2 * a2 + 1]);
+        }
+      }
+      int ac;
+      const double v = reduce_scatter_g<AP, 16>(acc, l, ac);
+      const int a = ch * AP + ac;
+      if (row < N && a < A && writer) {
+        const double m = v + sK[0][a];
+        const double d = act[row * A + a] - m;
+        mu_out[row * A + a] = m;
+        term += -0.5 * (sK[1][a] + d * d * sK[2][a]);
+      }
     }
     // logp_row = sum over the row's 16 lanes (non-writers hold 0)
 #pragma unroll
@@ -319,6 +329,123 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
   for (int c = threadIdx.x; c < H; c += blockDim.x) rec[A * H + 2 * A + c] = sRed[AP * 64 * NC + c];
 }
 
+// Backward for wide action spaces (8 < A <= 32: Humanoid 17, HandReach 20).  The per-lane dWm
+// accumulators of head_bwd_kernel would be NC x A doubles (5 x 24 at H = 300: over the register
+// file), so here the block's 256 lanes split the columns of one row (c = tid + 256 j, j < NC)
+// and every wave accumulates NC x AP values.  dmu is lane-distributed (lane a holds component a)
+// and broadcast with v_readlane; Wm sits in LDS as [a][Hs] (Hs = H rounded up to 64, dynamic
+// LDS, AP * Hs doubles).  The block walks rows i = blockIdx.x, += gridDim.x (fixed order), so
+// each block's partial record [dW (A*H) | db (A) | dls (A) | dbz (H)] is deterministic and
+// reduce_partials_kernel sums the records in a fixed order as for head_bwd_kernel.
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+template <int AP, int NC>
+__global__ __launch_bounds__(256) void head_bwd_wide_kernel(
+    const double* __restrict__ gl, const double* __restrict__ z, int64_t N, int H, int Hs,
+    const double* __restrict__ bz, const double* __restrict__ Wm, const double* __restrict__ log_std,
+    const double* __restrict__ act, const double* __restrict__ mu, int A,
+    double* __restrict__ dz, double* __restrict__ part) {
+  extern __shared__ double sWd[];  // [a < AP][c < Hs]
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  for (int e = tid; e < AP * Hs; e += blockDim.x) {
+    const int a = e / Hs, c = e % Hs;
+    sWd[e] = (a < A && c < H) ? Wm[a * H + c] : 0.0;
+  }
+  double inv = 0.0, es3 = 0.0;  // lane a (< A): 1/sigma_a^2, exp(ls)/sigma^3
+  if (l < A) {
+    const double e = exp(log_std[l]);
+    const double sd = e + kStdEps;
+    inv = 1.0 / (sd * sd);
+    es3 = e / (sd * sd * sd);
+  }
+  __syncthreads();
+  // wave-uniform: does this wave own any valid column in slot j?
+  bool live[NC];
+  double bzr[NC], accz[NC], accW[NC][AP];
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    live[j] = (w * 64 + 256 * j) < H;
+    const int c = tid + 256 * j;
+    bzr[j] = (bz && c < H) ? bz[c] : 0.0;
+    accz[j] = 0.0;
+#pragma unroll
+    for (int a = 0; a < AP; ++a) accW[j][a] = 0.0;
+  }
+  double accb = 0.0, accls = 0.0;
+  const int64_t last = N - 1;
+  const int la = l < A ? l : A - 1;
+  struct Slot {
+    double z[NC];
+    double g, av, mv;
+  };
+  auto load_slot = [&](Slot& s, int64_t i) {
+    const int64_t ic = i < N ? i : last;
+    const double* zr = z + ic * H;
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      const int c = tid + 256 * j;
+      s.z[j] = zr[c < H ? c : H - 1];
+    }
+    s.g = gl[ic];
+    s.av = act[ic * A + la];
+    s.mv = mu[ic * A + la];
+  };
+  Slot cur;
+  const int64_t i0 = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
+  load_slot(cur, i0);
+  for (int64_t i = i0; i < N; i += gridDim.x) {
+    Slot s = cur;
+    load_slot(cur, i + gridDim.x);
+    const double d = (l < A) ? s.av - s.mv : 0.0;
+    const double dm = s.g * d * inv;  // 0 for lanes >= A
+    if (l < A) {
+      accb += dm;
+      accls += s.g * (-1.0 + d * d * es3);
+    }
+    int cl = tid;
+    asm volatile("" : "+v"(cl));  // keep the Wm LDS reads in the loop
+#pragma unroll
+    for (int j = 0; j < NC; ++j) {
+      if (!live[j]) continue;
+      const int c = tid + 256 * j;
+      const double zb = s.z[j] + bzr[j];
+      const double x = fmax(zb, 0.0);
+      double dh = 0.0;
+#pragma unroll
+      for (int a = 0; a < AP; ++a) {
+        const double sa = readlane_d(dm, a);
+        dh = fma(sa, sWd[a * Hs + cl + 256 * j], dh);
+        accW[j][a] = fma(sa, x, accW[j][a]);
+      }
+      const double dzv = (zb > 0.0) ? dh : 0.0;
+      accz[j] += dzv;
+      if (dz && c < H) dz[i * H + c] = dzv;
+    }
+  }
+  const int64_t m = (int64_t)A * H + 2 * A + H;
+  double* rec = part + (int64_t)blockIdx.x * m;
+#pragma unroll
+  for (int j = 0; j < NC; ++j) {
+    const int c = tid + 256 * j;
+    if (c < H) {
+#pragma unroll
+      for (int a = 0; a < AP; ++a)
+        if (a < A) rec[a * H + c] = accW[j][a];
+      rec[A * H + 2 * A + c] = accz[j];
+    }
+  }
+  // db / dlog_std: every wave accumulated the same rows' components; wave 0 writes
+  if (w == 0 && l < A) {
+    rec[A * H + l] = accb;
+    rec[A * H + A + l] = accls;
+  }
+}
+
 // out = sum_b part[b][:] in a fixed order: 64 elements per block, wave w sums a quarter of the
 // partials, the 4 quarter sums are added in order.  dW goes to dWm, the tail to dbm / dls.
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __restrict__ part,
@@ -367,25 +494,28 @@ extern "C" int mepol_head_forward(const double* z, int64_t n, int hidden, const 
                                   void* stream) {
   if (n < 0 || hidden <= 0 || hidden > 64 * kMaxCols || a_dim <= 0 || a_dim > kMaxA || !z ||
       !Wm || !bm || !log_std || !act || !mu_out || !logp_out) {
-    set_error("mepol_head_forward: bad arguments (hidden <= 512, action_dim <= 8)");
+    set_error("mepol_head_forward: bad arguments (hidden <= 512, action_dim <= 32)");
     return kErrBadArg;
   }
   if (n == 0) return 0;
   const int ap = a_dim <= 1 ? 1 : a_dim <= 2 ? 2 : a_dim <= 4 ? 4 : 8;
+  const int nch = (a_dim + 7) / 8;  // chunks of 8 actions (a_dim > 8)
   const int ncl16 = (hidden + 15) / 16;
   const int ncl = ncl16 <= 4 ? 4 : ncl16 <= 8 ? 8 : ncl16 <= 12 ? 12 : ncl16 <= 16 ? 16
                 : ncl16 <= 20 ? 20 : ncl16 <= 24 ? 24 : 32;
   const int64_t groups = (n + 3) / 4;
   dim3 g((unsigned)std::max<int64_t>(1, std::min<int64_t>(1024, (groups / 4 + 3) / 4)));
   hipStream_t st = (hipStream_t)stream;
-#define MEPOL_HEAD_FWD(AP_, NC_)                                                                 \
-  if (ap == AP_ && ncl == NC_)                                                                   \
-    hipLaunchKernelGGL((head_fwd16_kernel<AP_, NC_>), g, dim3(256), 0, st, z, n, hidden, bz, Wm, \
-                       bm, log_std, act, a_dim, mu_out, logp_out);
-#define MEPOL_HEAD_FWD_A(AP_)                                                               \
-  MEPOL_HEAD_FWD(AP_, 4) MEPOL_HEAD_FWD(AP_, 8) MEPOL_HEAD_FWD(AP_, 12) MEPOL_HEAD_FWD(AP_, 16) \
-  MEPOL_HEAD_FWD(AP_, 20) MEPOL_HEAD_FWD(AP_, 24) MEPOL_HEAD_FWD(AP_, 32)
-  MEPOL_HEAD_FWD_A(1) MEPOL_HEAD_FWD_A(2) MEPOL_HEAD_FWD_A(4) MEPOL_HEAD_FWD_A(8)
+#define MEPOL_HEAD_FWD(AP_, NC_, NCH_)                                                       \
+  if (ap == AP_ && ncl == NC_ && nch == NCH_)                                                \
+    hipLaunchKernelGGL((head_fwd16_kernel<AP_, NC_, NCH_>), g, dim3(256), 0, st, z, n, hidden, \
+                       bz, Wm, bm, log_std, act, a_dim, mu_out, logp_out);
+#define MEPOL_HEAD_FWD_A(AP_, NCH_)                                                    \
+  MEPOL_HEAD_FWD(AP_, 4, NCH_) MEPOL_HEAD_FWD(AP_, 8, NCH_) MEPOL_HEAD_FWD(AP_, 12, NCH_) \
+  MEPOL_HEAD_FWD(AP_, 16, NCH_) MEPOL_HEAD_FWD(AP_, 20, NCH_) MEPOL_HEAD_FWD(AP_, 24, NCH_) \
+  MEPOL_HEAD_FWD(AP_, 32, NCH_)
+  MEPOL_HEAD_FWD_A(1, 1) MEPOL_HEAD_FWD_A(2, 1) MEPOL_HEAD_FWD_A(4, 1) MEPOL_HEAD_FWD_A(8, 1)
+  MEPOL_HEAD_FWD_A(8, 2) MEPOL_HEAD_FWD_A(8, 3) MEPOL_HEAD_FWD_A(8, 4)
 #undef MEPOL_HEAD_FWD_A
 #undef MEPOL_HEAD_FWD
   MEPOL_CHECK_LAUNCH();
@@ -420,6 +550,32 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
   }
   hipStream_t st = (hipStream_t)stream;
   double* pdW = (double*)workspace;
+  if (a_dim > 8) {
+    const int apw = a_dim <= 16 ? 16 : a_dim <= 24 ? 24 : 32;
+    const int ncw = (hidden + 255) / 256;
+    const int hs = (hidden + 63) / 64 * 64;
+    const size_t lds = (size_t)apw * hs * sizeof(double);
+#define MEPOL_HEAD_BWDW(AP_, NC_)                                                               \
+  if (apw == AP_ && ncw == NC_) {                                                               \
+    static bool attr_set = false;                                                               \
+    if (!attr_set) {                                                                            \
+      MEPOL_HIP(hipFuncSetAttribute((const void*)head_bwd_wide_kernel<AP_, NC_>,                \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));   \
+      attr_set = true;                                                                          \
+    }                                                                                           \
+    hipLaunchKernelGGL((head_bwd_wide_kernel<AP_, NC_>), dim3(nb), dim3(256), lds, st, grad_logp, \
+                       z, n, hidden, hs, bz, Wm, log_std, act, mu, a_dim, dz, pdW);             \
+  }
+    MEPOL_HEAD_BWDW(16, 1) MEPOL_HEAD_BWDW(16, 2) MEPOL_HEAD_BWDW(24, 1) MEPOL_HEAD_BWDW(24, 2)
+    MEPOL_HEAD_BWDW(32, 1) MEPOL_HEAD_BWDW(32, 2)
+#undef MEPOL_HEAD_BWDW
+    MEPOL_CHECK_LAUNCH();
+    const int64_t m = (int64_t)a_dim * hidden + 2 * a_dim + hidden;
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st,
+                       pdW, nb, m, a_dim * hidden, a_dim, dWm, dbm, dlog_std, dbz);
+    MEPOL_CHECK_LAUNCH();
+    return 0;
+  }
   const int nc = (hidden + 63) / 64;
   const int ap = a_dim <= 1 ? 1 : a_dim <= 2 ? 2 : a_dim <= 4 ? 4 : 8;
   dim3 g(nb);

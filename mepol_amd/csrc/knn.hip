@@ -268,19 +268,42 @@ __global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ a
 //     are unscaled exactly.  refine's certification uses this path's error bound.
 // ---------------------------------------------------------------------------------------
 // max |x| over candidates (scal[0]) and over queries (scal[2]), non-negative float bit order.
+// Input validation (sklearn's check_array inside NearestNeighbors.fit / kneighbors,
+// mepol.py:190-192): rows with a NaN / inf coordinate are counted in bad[0], rows whose f32
+// squared norm overflows (|x| >~ 1.8e19) in bad[1].  The tests are on laundered bit patterns: this
+// TU is built with -fno-honor-nans (for the selection kernels), under which the compiler rewrites
+// a plain exponent test into |x| == inf and loses NaN.  Once validated, no NaN reaches the
+// selection / refine / exact kernels, so the flag cannot change their results.
+__device__ __forceinline__ bool nonfinite_bits(float v) {
+  unsigned b = __float_as_uint(v);
+  asm volatile("" : "+v"(b));
+  return (b & 0x7f800000u) == 0x7f800000u;
+}
+
 __global__ __launch_bounds__(256) void norms_kernel(const float* __restrict__ X, int64_t n, int d,
-                                                    unsigned* __restrict__ out_bits) {
+                                                    unsigned* __restrict__ out_bits,
+                                                    unsigned* __restrict__ bad) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float nrm = 0.f;
+  bool nonfinite = false, overflow = false;
   if (i < n) {
     const float* x = X + i * d;
     float s2 = 0.f;
-    for (int f = 0; f < d; ++f) s2 = fmaf(x[f], x[f], s2);
-    nrm = sqrtf(s2);
+    for (int f = 0; f < d; ++f) {
+      nonfinite |= nonfinite_bits(x[f]);
+      s2 = fmaf(x[f], x[f], s2);
+    }
+    overflow = !nonfinite && nonfinite_bits(s2);
+    nrm = (nonfinite || overflow) ? 0.f : sqrtf(s2);
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) nrm = fmaxf(nrm, __shfl_xor(nrm, m, kWave));
   if ((threadIdx.x & 63) == 0) atomicMax(out_bits, __float_as_uint(nrm));
+  const unsigned long long b1 = __ballot(nonfinite), b2 = __ballot(overflow);
+  if ((threadIdx.x & 63) == 0) {
+    if (b1) atomicAdd(bad, (unsigned)__popcll(b1));
+    if (b2) atomicAdd(bad + 1, (unsigned)__popcll(b2));
+  }
 }
 
 // sigma = 2^e with sigma * max(cmax, qmax) in (64, 128] (1 when the data is all zero).
@@ -1103,8 +1126,8 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   off = align_up(off + std::max((size_t)P->nct * 64 * P->KSP * sizeof(float),
                                 (size_t)P->nct * 64 * P->KS16 * 16 * sizeof(_Float16)),
                  256);
-  P->off_scalars = off;
-  off = align_up(off + 16, 256);
+  P->off_scalars = off;  // [0] max |c| bits, [1] fallback count, [2] max |q| bits, [4..5] invalid rows
+  off = align_up(off + 32, 256);
   const size_t nl = (size_t)std::max<int64_t>(nq, 1) * P->M;
   P->off_lv = off;
   off = align_up(off + nl * sizeof(float), 256);
@@ -1256,14 +1279,30 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
 
   float* tau = nullptr;   // sampled per-query bounds (mode 1 with sampling)
   int* counts = nullptr;  // survivors per query (filter pass)
-  MEPOL_HIP(hipMemsetAsync(ws + P.off_scalars, 0, 16, st));
+  MEPOL_HIP(hipMemsetAsync(ws + P.off_scalars, 0, 32, st));
   if (n_fallback_out) MEPOL_HIP(hipMemsetAsync(n_fallback_out, 0, sizeof(int32_t), st));
+  // scal[0] = max candidate norm (refine's C), scal[2] = max query norm (split-f16 scale)
+  hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nc + 255) / 256)), dim3(256), 0, st, cand,
+                     P.nc, P.d, cmax, cmax + 4);
+  hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nq + 255) / 256)), dim3(256), 0, st, query,
+                     P.nq, P.d, cmax + 2, cmax + 4);
+  MEPOL_CHECK_LAUNCH();
+  {
+    // sklearn rejects non-finite input (ValueError from check_array): validate before the scan.
+    // One stream synchronisation per call, like the reference's blocking kneighbors.
+    unsigned bad[2] = {0, 0};
+    MEPOL_HIP(hipMemcpyAsync(bad, cmax + 4, sizeof(bad), hipMemcpyDeviceToHost, st));
+    MEPOL_HIP(hipStreamSynchronize(st));
+    if (bad[0]) {
+      set_error("mepol_knn: Input contains NaN or infinity (%u rows)", bad[0]);
+      return kErrBadArg;
+    }
+    if (bad[1]) {
+      set_error("mepol_knn: %u rows have a squared norm beyond float32 range", bad[1]);
+      return kErrUnsupported;
+    }
+  }
   if (P.mode == 1) {
-    // scal[0] = max candidate norm (refine's C), scal[2] = max query norm (scale only)
-    hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nc + 255) / 256)), dim3(256), 0, st, cand,
-                       P.nc, P.d, cmax);
-    hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nq + 255) / 256)), dim3(256), 0, st, query,
-                       P.nq, P.d, cmax + 2);
     _Float16* ap16 = (_Float16*)apack;
     const int64_t total = P.nct * 64;
     hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,

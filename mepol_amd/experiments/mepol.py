@@ -116,7 +116,26 @@ def main(argv=None):
         print("mepol_amd needs a ROCm GPU (MI355X); there is no CPU path.")
         return 3
     torch.set_default_dtype(torch.float64)
-    device = torch.device("cuda")
+    # One process per GPU under torch.distributed.run (WORLD_SIZE > 1): mepol() shards the
+    # particle batch over the ranks (RCCL; gloo when ranks share a GPU).  Rank 0 picks the
+    # results directory and the seed and shares them.
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        ndev = torch.cuda.device_count()
+        local = int(os.environ.get("LOCAL_RANK", "0")) % ndev
+        torch.cuda.set_device(local)
+        if not dist.is_initialized():
+            if ndev >= world:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("gloo")
+        device = torch.device("cuda", local)
+    else:
+        device = torch.device("cuda")
+    rank = dist.get_rank() if dist is not None else 0
     env = spec["env_create"]()
     state_filter = spec.get("state_filter")
     eps = spec["eps"]
@@ -140,8 +159,9 @@ def main(argv=None):
     root = args.results_dir or os.path.join(os.getcwd(), "results", "exploration")
     out_path = os.path.join(root, args.tb_dir_name, exp_name + "__" +
                             datetime.now().strftime("%Y_%m_%d_%H_%M_%S") + "__" + str(os.getpid()))
-    os.makedirs(out_path, exist_ok=True)
-    with open(os.path.join(out_path, "log_info.txt"), "w") as f:
+    if rank == 0:
+        os.makedirs(out_path, exist_ok=True)
+    with open(os.path.join(out_path, "log_info.txt") if rank == 0 else os.devnull, "w") as f:
         f.write("Run info:\n")
         f.write("-" * 10 + "\n")
         for key, value in vars(args).items():
@@ -152,6 +172,10 @@ def main(argv=None):
         if args.seed is None:
             args.seed = int(np.random.randint(2 ** 16 - 1))
             f.write(f"Setting random seed {args.seed}\n")
+    if dist is not None:
+        shared = [out_path, args.seed]
+        dist.broadcast_object_list(shared, src=0)
+        out_path, args.seed = shared
 
     mepol(env=env, env_name=args.env, state_filter=state_filter, create_policy=create_policy,
           k=args.k, kl_threshold=args.kl_threshold, max_off_iters=args.max_off_iters,
@@ -166,6 +190,8 @@ def main(argv=None):
           heatmap_cmap=spec.get("heatmap_cmap"), heatmap_labels=spec.get("heatmap_labels"),
           heatmap_interp=spec.get("heatmap_interp"), seed=args.seed, out_path=out_path,
           num_workers=args.num_workers)
+    if dist is not None:
+        dist.barrier()
     return 0
 
 

@@ -32,12 +32,34 @@ def _require_device(*ts):
 
 
 def _workspace(device, nbytes, tag="knn"):
-    key = (tag, device)
+    """Scratch for eager calls, one buffer per (tag, device, stream): calls on one stream are
+    ordered, so they may share it; a buffer outgrown on a stream is released through the caching
+    allocator, which is stream-aware.  Captured graphs (algorithms/device_loop.py) never use this
+    cache: they own their scratch (see head_workspace / layer_workspace)."""
+    key = (tag, device, torch.cuda.current_stream(device).cuda_stream)
     buf = _WS.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
         _WS[key] = buf
     return buf
+
+
+def head_workspace(n, hidden, a, device):
+    """A caller-owned scratch buffer for head_backward at these sizes."""
+    import ctypes
+
+    nbytes = ctypes.c_size_t()
+    call("mepol_head_workspace_size", n, hidden, a, ctypes.byref(nbytes))
+    return torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=device)
+
+
+def layer_workspace(n, f, out, device):
+    """A caller-owned scratch buffer for layer_backward at these sizes."""
+    import ctypes
+
+    nbytes = ctypes.c_size_t()
+    call("mepol_layer_workspace_size", n, f, out, ctypes.byref(nbytes))
+    return torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=device)
 
 
 def knn_plan(n_cand, n_query, d, kp1, split=0):
@@ -197,16 +219,18 @@ def head_forward(z, Wm, bm, log_std, act, bz=None, mu_out=None, logp_out=None):
     return mu, logp
 
 
-def head_backward(grad_logp, z, Wm, log_std, act, mu, bz=None, need_dz=True):
-    """Returns (dz or None, dWm, dbm, dlog_std, dbz or None)."""
+def head_backward(grad_logp, z, Wm, log_std, act, mu, bz=None, need_dz=True, ws=None):
+    """Returns (dz or None, dWm, dbm, dlog_std, dbz or None).  `ws`: caller-owned scratch
+    (head_workspace); default: the per-stream eager cache."""
     import ctypes
 
     n, h = z.shape
     a = Wm.shape[0]
     dev = z.device
-    nbytes = ctypes.c_size_t()
-    call("mepol_head_workspace_size", n, h, a, ctypes.byref(nbytes))
-    ws = _workspace(dev, nbytes.value, tag="head")
+    if ws is None:
+        nbytes = ctypes.c_size_t()
+        call("mepol_head_workspace_size", n, h, a, ctypes.byref(nbytes))
+        ws = _workspace(dev, nbytes.value, tag="head")
     dz = torch.empty_like(z) if need_dz else None
     dWm = torch.empty_like(Wm)
     dbm = torch.empty(a, dtype=torch.float64, device=dev)
@@ -227,15 +251,17 @@ def layer_forward(x, W, b, out=None):
     return h
 
 
-def layer_backward(dh, h, x):
-    """(dW, db) of h = relu(x W^T + b) from dL/dh and the forward output h."""
+def layer_backward(dh, h, x, ws=None):
+    """(dW, db) of h = relu(x W^T + b) from dL/dh and the forward output h.  `ws`: caller-owned
+    scratch (layer_workspace); default: the per-stream eager cache."""
     import ctypes
 
     n, f = x.shape
     out = h.shape[1]
-    nbytes = ctypes.c_size_t()
-    call("mepol_layer_workspace_size", n, f, out, ctypes.byref(nbytes))
-    ws = _workspace(x.device, nbytes.value, tag="layer")
+    if ws is None:
+        nbytes = ctypes.c_size_t()
+        call("mepol_layer_workspace_size", n, f, out, ctypes.byref(nbytes))
+        ws = _workspace(x.device, nbytes.value, tag="layer")
     dW = torch.empty((out, f), dtype=torch.float64, device=x.device)
     db = torch.empty(out, dtype=torch.float64, device=x.device)
     call("mepol_layer_backward", ptr(dh), ptr(h), ptr(x), n, f, out, ptr(dW), ptr(db), ptr(ws),

@@ -308,10 +308,10 @@ class ShardedIteration(DeviceIteration):
         grad = ops.entropy_reverse_scan(gamma, w_local, partials, nparts, self.offsets, nt, T,
                                         self.neg_one, S_ext=S)
         dz2, dWm, dbm, dls, db2 = ops.head_backward(grad.view(-1), self.z2, Wm, ls, self.act,
-                                                    self.mu, bz=b2, need_dz=True)
+                                                    self.mu, bz=b2, need_dz=True, ws=self.ws_head)
         dW2 = _weight_grad(dz2, self.h1)
         dh1 = torch.mm(dz2, W2)
-        dW1, db1 = ops.layer_backward(dh1, self.h1, self.x)
+        dW1, db1 = ops.layer_backward(dh1, self.h1, self.x, ws=self.ws_layer)
         grad_of = {id(p): t for p, t in zip(self.named, (dW1, db1, dW2, db2, dWm, dbm, dls))}
         flat = torch.cat([grad_of[id(p)].reshape(-1) for p in self.params])
         self.dist.all_reduce(flat, group=self.group)  # ShardedEpoch.allreduce_grads

@@ -150,7 +150,7 @@ class GaussianPolicy(nn.Module):
 
     def _fused_head_ok(self, states, actions):
         return (states.is_cuda and states.dim() == 2 and states.shape[0] >= SPLITK_MIN_ROWS
-                and self.activation is nn.ReLU and self.action_dim <= 8
+                and self.activation is nn.ReLU and self.action_dim <= 32
                 and self.mean.in_features <= 512 and states.dtype == torch.float64
                 and actions.dtype == torch.float64)
 

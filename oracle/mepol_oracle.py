@@ -48,6 +48,39 @@ def knn_exact(X, kp1, Q=None, chunk=512):
     return D, I
 
 
+def knn_exact_sampled(X, kp1, Q, chunk=64):
+    """knn_exact for a few queries Q against a large candidate set X (N up to 500k).
+
+    Same result as knn_exact (feature-order f64 distances, (distance, index) order); the
+    candidates are pre-screened with the f64 GEMM form |q|^2 + |x|^2 - 2 q.x, whose error is
+    below (d + 4) * 2^-52 * (|q| + |x|)^2 <= tol (Higham's dot-product bound with margin), so
+    every candidate whose exact d^2 is at most the kp1-th exact value survives the screen:
+    approx(c) <= exact(c) + tol <= exact_kp1 + tol <= approx_kp1 + 2 tol."""
+    X = np.asarray(X, dtype=np.float32).astype(np.float64)
+    Q = np.asarray(Q, dtype=np.float32).astype(np.float64)
+    n, d = X.shape
+    xn = np.einsum("ij,ij->i", X, X)
+    qn = np.einsum("ij,ij->i", Q, Q)
+    scale = (np.sqrt(qn).max() + np.sqrt(xn).max()) ** 2
+    tol = (d + 4) * 2.0 ** -52 * scale * 4
+    D = np.empty((Q.shape[0], kp1), dtype=np.float64)
+    I = np.empty((Q.shape[0], kp1), dtype=np.int64)
+    for s in range(0, Q.shape[0], chunk):
+        q = Q[s:s + chunk]
+        approx = qn[s:s + chunk, None] + xn[None, :] - 2.0 * (q @ X.T)
+        kth = np.partition(approx, kp1 - 1, axis=1)[:, kp1 - 1]
+        for r in range(q.shape[0]):
+            cand = np.nonzero(approx[r] <= kth[r] + 2 * tol)[0]
+            acc = np.zeros(cand.shape[0])
+            for f in range(d):
+                t = q[r, f] - X[cand, f]
+                acc += t * t
+            order = np.lexsort((cand, acc))[:kp1]
+            D[s + r] = np.sqrt(acc[order])
+            I[s + r] = cand[order]
+    return D, I
+
+
 def knn_sklearn(X, kp1, n_jobs=1, algorithm="auto"):
     """The reference call itself (mepol.py:190-192) -- used as the timed CPU baseline."""
     from sklearn.neighbors import NearestNeighbors

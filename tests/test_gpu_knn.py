@@ -107,3 +107,45 @@ def test_knn_large_properties(cuda):
     Dq, Iq, _ = ops.knn_exact(X, 31, query=X[sel[:64]])
     assert torch.equal(Dq, D[sel[:64]]) and torch.equal(Iq, I[sel[:64]])
     assert int(nfb.item()) < 200  # certification almost never needs the exhaustive path
+
+
+@pytest.mark.parametrize("n,d,kp1", [(200000, 29, 31), (200000, 47, 31), (500000, 63, 51)],
+                         ids=["C3", "C4", "C5"])
+def test_knn_config_sizes_vs_oracle(cuda, n, d, kp1):
+    """BASELINE sizes (C3 Ant d=29 k=30, C4 Humanoid d=47 k=30, C5 HandReach N=500k d=63
+    k=50) on one GPU: 512 sampled query rows bit-exact against the CPU oracle's exhaustive
+    scan (O.knn_exact_sampled), every row sorted with self first."""
+    from mepol_amd import ops
+
+    rng = np.random.default_rng(d)
+    X = rng.standard_normal((n, d)).astype(np.float32)
+    Xt = torch.as_tensor(X, device="cuda")
+    D, I, I32T, nfb = ops.knn(Xt, kp1, return_fallback=True)
+    torch.cuda.synchronize()
+    assert bool((D[:, 1:] >= D[:, :-1]).all())
+    assert bool((I[:, 0] == torch.arange(n, device="cuda")).all())
+    assert torch.equal(I32T.t().long(), I)
+    sel = np.sort(rng.choice(n, 512, replace=False))
+    Do, Io = O.knn_exact_sampled(X, kp1, X[sel])
+    assert np.array_equal(D[torch.as_tensor(sel, device="cuda")].cpu().numpy(), Do)
+    assert np.array_equal(I[torch.as_tensor(sel, device="cuda")].cpu().numpy(), Io)
+    assert int(nfb.item()) < n // 1000
+
+
+@pytest.mark.parametrize("bad", [np.nan, np.inf, -np.inf])
+@pytest.mark.parametrize("where", ["cand", "query"])
+def test_knn_rejects_non_finite(cuda, bad, where):
+    """sklearn's NearestNeighbors.fit / kneighbors raise ValueError on NaN / inf
+    (mepol.py:190-192); the C ABI returns MEPOL_ERR_BAD_ARG, raised as a ValueError."""
+    from mepol_amd import ops
+
+    X = np.random.default_rng(0).standard_normal((2000, 29)).astype(np.float32)
+    Q = X[:300].copy()
+    (X if where == "cand" else Q)[123, 7] = bad
+    with pytest.raises(ValueError, match="NaN or infinity"):
+        ops.knn(torch.as_tensor(X, device="cuda"), 31, query=torch.as_tensor(Q, device="cuda"))
+    # the library stays usable after the rejection
+    X[123, 7] = 0.5
+    D, I, _ = ops.knn(torch.as_tensor(X, device="cuda"), 31)
+    Do, Io = O.knn_exact(X, 31)
+    assert np.array_equal(D.cpu().numpy(), Do) and np.array_equal(I.cpu().numpy(), Io)

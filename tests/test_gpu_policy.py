@@ -6,7 +6,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("nf,hidden,a", [(2, [300, 300], 2), (2, [300, 300], 1), (29, [400, 300], 8),
-                                         (7, [64, 100], 3), (5, [33], 4)])
+                                         (7, [64, 100], 3), (5, [33], 4), (47, [400, 300], 17),
+                                         (63, [400, 300], 20), (5, [33], 12), (7, [64, 100], 32),
+                                         (9, [70, 500], 24)])
 def test_fused_head_matches_unfused(cuda, nf, hidden, a):
     from mepol_amd import policy as P
 
@@ -33,7 +35,9 @@ def test_fused_head_matches_unfused(cuda, nf, hidden, a):
         assert torch.allclose(pol.get_log_p(s, act), ref, rtol=1e-12, atol=1e-12)
 
 
-@pytest.mark.parametrize("nf,hidden,a", [(29, [400, 300], 8), (2, [300, 300], 2), (7, [130, 70], 3)])
+@pytest.mark.parametrize("nf,hidden,a", [(29, [400, 300], 8), (2, [300, 300], 2), (7, [130, 70], 3),
+                                         (47, [400, 300], 17), (63, [400, 300], 20),
+                                         (11, [96, 260], 32)])
 def test_two_layer_fused_path_matches_nn_modules(cuda, nf, hidden, a):
     """The _TwoLayerLogp path (HIP layer 1 + rocBLAS layer 2 + HIP head) == nn.Linear/ReLU."""
     from mepol_amd import policy as P
@@ -56,3 +60,20 @@ def test_two_layer_fused_path_matches_nn_modules(cuda, nf, hidden, a):
     assert torch.allclose(lp, ref, rtol=1e-12, atol=1e-12)
     for k, v in pol.named_parameters():
         assert torch.allclose(got[k], v.grad, rtol=1e-10, atol=1e-12 * v.grad.abs().max()), k
+
+
+def test_predict_matches_forward(cuda):
+    """predict (policy.py:64-67): batch-1, no grad, returns out[0] on the CPU; deterministic
+    gives the mean of the batched forward."""
+    from mepol_amd import policy as P
+
+    torch.manual_seed(3)
+    pol = P.GaussianPolicy([300, 300], 2, 2, -1.5).cuda()
+    s = [0.25, -1.5]
+    a = pol.predict(s, deterministic=True)
+    assert a.device.type == "cpu" and a.shape == (2,) and a.dtype == torch.float64
+    mu, _ = pol(torch.tensor([s], dtype=torch.float64, device="cuda"), deterministic=True)
+    assert torch.equal(a, mu[0].cpu())
+    torch.manual_seed(0)
+    b = pol.predict(s)
+    assert b.shape == (2,) and not torch.equal(a, b)

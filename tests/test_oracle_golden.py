@@ -25,6 +25,19 @@ def test_knn_oracle_matches_reference(name):
     assert np.array_equal(I, z["I"].astype(np.int64))
 
 
+@pytest.mark.parametrize("name", KNN_TIE_FREE + ["knn_gw_ties"])
+def test_knn_sampled_oracle_equals_exhaustive(name):
+    """The GEMM-screened sampled-query oracle (used at the BASELINE sizes on the GPU box) returns
+    exactly knn_exact's rows, ties and duplicates included."""
+    z = load_golden(name)
+    X = z["X"]
+    kp1 = int(z["kp1"])
+    sel = np.random.default_rng(0).choice(X.shape[0], 97, replace=False)
+    D, I = O.knn_exact(X, kp1, Q=X[sel])
+    Ds, Is = O.knn_exact_sampled(X, kp1, X[sel], chunk=13)
+    assert np.array_equal(D, Ds) and np.array_equal(I, Is)
+
+
 @pytest.mark.parametrize("name", ["knn_gw_ties", "knn_gw_c2"])
 def test_knn_oracle_ties_tie_invariant(name):
     """Real GridWorld particles have exact duplicates: compare what tie order cannot change."""
