@@ -240,19 +240,27 @@ class DeviceIteration:
         out_k, _, _ = ops.entropy_forward(w2, self.idx32T, self.D, k, 1.0, 1.0, 0.0, self.eps)
         torch.cat((out_h[:1], out_k[1:2]), out=self.vals)
 
-    def _capture(self):
+    def _warmup(self):
+        """One eager pass on a side stream (allocator pools, library handles, kernel code)."""
         cur = torch.cuda.current_stream()
-        side = torch.cuda.Stream(device=self.device)
+        self._side = torch.cuda.Stream(device=self.device)
         self.scal.zero_()  # enable = 0: the warm-up pass leaves theta and the moments untouched
-        side.wait_stream(cur)
-        with torch.cuda.stream(side):
+        self._side.wait_stream(cur)
+        with torch.cuda.stream(self._side):
             self._body()
-        cur.wait_stream(side)
+        cur.wait_stream(self._side)
+
+    def _capture_graph(self):
+        cur = torch.cuda.current_stream()
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=side):
+        with torch.cuda.graph(graph, stream=self._side):
             self._body()
-        cur.wait_stream(side)
+        cur.wait_stream(self._side)
         self.graph = graph
+
+    def _capture(self):
+        self._warmup()
+        self._capture_graph()
 
     def step(self):
         """policy_update + compute_kl.  Returns host floats (H(theta_t), KL(theta_t+1)

@@ -331,9 +331,15 @@ class ShardedIteration(DeviceIteration):
         torch.stack((H, KL), out=self.vals)
 
     def try_capture(self):
+        """Capture the iteration; all ranks agree on graph or eager.  The warm-up pass issues
+        real collectives, so it runs outside the fallback: a failure there is an error on that
+        rank (raised), not a reason to fall back, because the other ranks would otherwise wait
+        in a collective it never joins.  Only the capture itself -- collectives are recorded,
+        not executed -- may fail over to the eager path, by consensus (MIN of a flag)."""
+        self._warmup()
         ok = 1
         try:
-            self._capture()
+            self._capture_graph()
         except Exception:  # capture unsupported here: every rank falls back together
             self.graph = None
             ok = 0
