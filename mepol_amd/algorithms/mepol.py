@@ -21,6 +21,7 @@ Differences a caller can observe (all documented in DESIGN.md):
 import math
 import os
 import time
+import weakref
 
 import numpy as np
 import scipy.special
@@ -39,6 +40,74 @@ int_type = torch.int64
 # ---------------------------------------------------------------------------------------------
 def _batched_kind(env):
     return getattr(type(unwrap(env)), "batched_kind", None)
+
+
+class _RolloutGraph:
+    """The T-step rollout of a HIP-stepped env as one replayed HIP graph.
+
+    Each step is the policy MLP (a few small GEMM / ReLU launches) plus the fused
+    rollout_step kernel: at MEPOL's batch sizes (tens to hundreds of trajectories) the loop is
+    launch-bound (~65 us per step eager).  Captured once per (policy, env, shape) into static
+    buffers -- initial states, the pre-drawn noise [T, n, a], the recorded states / actions --
+    and replayed every epoch; the policy's parameters are read in place, so load_state_dict
+    between epochs needs no re-capture."""
+
+    def __init__(self, policy, env_id, init, T, a_dim, nf):
+        dev = init.device
+        n = init.shape[0]
+        self.key = (env_id, n, T, a_dim, nf, tuple(p.data_ptr() for p in policy.parameters()))
+        self.init = init.clone()
+        self.noise = torch.zeros((T, n, a_dim), dtype=torch.float64, device=dev)
+        self.states = torch.zeros((n, T + 1, nf), dtype=torch.float32, device=dev)
+        self.actions = torch.zeros((n, T, a_dim), dtype=torch.float32, device=dev)
+        self.env = torch.empty_like(init)
+        self.policy_in = torch.empty((n, nf), dtype=torch.float64, device=dev)
+        self.log_std = policy.log_std.detach()
+        # weak: the cache entry is keyed by the policy and must not keep it alive
+        self.env_id, self.T, self._policy = env_id, T, weakref.ref(policy)
+        # warm-up (library handles, workspaces) outside the capture, then capture
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            self._body(1)
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=side):
+            self._body(T)
+        torch.cuda.current_stream().wait_stream(side)
+
+    def _body(self, steps):
+        self.env.copy_(self.init)
+        self.policy_in.copy_(self.init)
+        self.states[:, 0].copy_(self.init)
+        e64 = self.env if self.env_id == 0 else None
+        e32 = self.env if self.env_id == 1 else None
+        for t in range(steps):
+            mean = self._policy().mean_action(self.policy_in).contiguous()
+            ops.rollout_step(self.env_id, e64, e32, mean, self.noise[t], self.log_std, t, self.T,
+                             self.states, self.actions, self.policy_in)
+
+    def run(self, init, noise):
+        self.init.copy_(init)
+        self.noise.copy_(noise)
+        self.graph.replay()
+        return self.states.clone(), self.actions.clone()
+
+
+_ROLLOUT_GRAPHS = weakref.WeakKeyDictionary()  # policy -> {key: _RolloutGraph}
+
+
+def _rollout_graph(policy, env_id, init, T, a_dim, nf):
+    if os.environ.get("MEPOL_ROLLOUT_GRAPH", "1") == "0" or not policy.log_std.is_contiguous():
+        return None
+    key = (env_id, init.shape[0], T, a_dim, nf, tuple(p.data_ptr() for p in policy.parameters()))
+    per = _ROLLOUT_GRAPHS.setdefault(policy, {})
+    g = per.get(key)
+    if g is None:
+        if len(per) >= 4:  # bounded: the epoch and full-entropy shapes of a run
+            per.clear()
+        g = per[key] = _RolloutGraph(policy, env_id, init, T, a_dim, nf)
+    return g
 
 
 def collect_particles_device(env, policy, num_traj, traj_len, state_filter, generator=None,
@@ -80,6 +149,14 @@ def collect_particles_device(env, policy, num_traj, traj_len, state_filter, gene
             init = base.reset_batch_torch(total, dev, generator)[lo:hi]
             noise_all = torch.randn((T, total, a_dim), dtype=torch.float64, device=dev,
                                     generator=generator)
+            graph = _rollout_graph(policy, env_id, init, T, a_dim, nf) if visited is None else None
+            if graph is not None:
+                states, actions = graph.run(init, noise_all[:, lo:hi])
+                rtl = torch.full((num_traj, 1), T, dtype=torch.int32, device=dev)
+                next_states = states[:, 1:, :].reshape(-1, nf)
+                if state_filter is not None:
+                    next_states = next_states[:, list(state_filter)]
+                return states, actions, rtl, next_states.contiguous()
             env64 = init.clone() if env_id == 0 else None
             env32 = init.clone() if env_id == 1 else None
             policy_in = init.to(torch.float64).contiguous()

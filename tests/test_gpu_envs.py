@@ -97,3 +97,42 @@ def test_collect_particles_contract(cuda):
     assert torch.equal(ns, st[:, 1:].reshape(-1, 2))
     Do, Io = O.knn_exact(ns.float().cpu().numpy(), 5)
     assert np.array_equal(D.cpu().numpy(), Do) and np.array_equal(I.cpu().numpy(), Io)
+
+
+@pytest.mark.parametrize("env_name", ["mountaincar", "gridworld"])
+def test_rollout_graph_and_shards_match_eager(cuda, monkeypatch, env_name):
+    """The graph-replayed rollout == the eager per-step loop (bitwise), and the shards of a
+    2- and 4-way trajectory split concatenate to the one-rank rollout (noise and initial states
+    are drawn for all trajectories up front)."""
+    from mepol_amd.algorithms import mepol as M
+    from mepol_amd.envs import ErgodicEnv, GridWorldContinuous, MountainCarContinuous
+    from mepol_amd.policy import GaussianPolicy
+
+    base = MountainCarContinuous() if env_name == "mountaincar" else GridWorldContinuous()
+    env = ErgodicEnv(base)
+    a = env.action_space.shape[0]
+    torch.manual_seed(0)
+    pol = GaussianPolicy([300, 300], 2, a, -1.0).cuda()
+
+    def roll(graph, shard=None, seed=7):
+        monkeypatch.setenv("MEPOL_ROLLOUT_GRAPH", "1" if graph else "0")
+        g = torch.Generator(device="cuda").manual_seed(seed)
+        return M.collect_particles_device(env, pol, 8, 300, None, generator=g, shard=shard)
+
+    eager = roll(False)
+    for rep in range(2):  # capture, then replay of the cached graph
+        graph = roll(True)
+        for x, y in zip(eager, graph):
+            assert torch.equal(x, y)
+    assert len(M._ROLLOUT_GRAPHS.get(pol, {})) == 1
+    for world in (2, 4):
+        parts = [roll(True, shard=(r, world)) for r in range(world)]
+        assert torch.equal(torch.cat([p[0] for p in parts]), eager[0])
+        assert torch.equal(torch.cat([p[1] for p in parts]), eager[1])
+        assert torch.equal(torch.cat([p[3] for p in parts]), eager[3])
+    # the parameters are read in place at replay: a changed policy changes the rollout
+    with torch.no_grad():
+        pol.mean.bias.add_(0.05)
+    eager2 = roll(False)
+    graph2 = roll(True)
+    assert torch.equal(eager2[0], graph2[0]) and not torch.equal(eager2[0], eager[0])

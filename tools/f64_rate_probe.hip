@@ -17,6 +17,19 @@ __global__ __launch_bounds__(256) void mfma_loop(double* out, int iters) {
   out[blockIdx.x * 256 + threadIdx.x] = s.x + s.y + s.z + s.w;
 }
 
+__global__ __launch_bounds__(256) void mfma_loop8(double* out, int iters) {
+  d4 c[8];
+  for (int j = 0; j < 8; ++j) c[j] = (d4){0, 0, 0, 0};
+  double a = threadIdx.x * 1e-3, b = 1.0 - threadIdx.x * 1e-4;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c[j], 0, 0, 0);
+  }
+  d4 s = c[0];
+  for (int j = 1; j < 8; ++j) s += c[j];
+  out[blockIdx.x * 256 + threadIdx.x] = s.x + s.y + s.z + s.w;
+}
+
 __global__ __launch_bounds__(256) void fma_loop(double* out, int iters) {
   double a[8];
   for (int j = 0; j < 8; ++j) a[j] = threadIdx.x * 1e-3 + j;
@@ -82,6 +95,12 @@ int main() {
     hipEventElapsedTime(&ms, e0, e1);
     double fl = (double)blocks * 4 * iters * 4 * 2048.0;
     printf("mfma_f64_16x16x4: %.3f ms  %.1f TF/s\n", ms, fl / ms / 1e9);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL(mfma_loop8, dim3(blocks), dim3(256), 0, 0, out, iters / 2);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("mfma_f64_16x16x4 (8 chains): %.3f ms  %.1f TF/s\n", ms, fl / ms / 1e9);
     hipEventRecord(e0);
     hipLaunchKernelGGL(fma_loop, dim3(blocks), dim3(256), 0, 0, out, iters);
     hipEventRecord(e1);
