@@ -408,20 +408,19 @@ def cpu_baseline(cfg, sample_queries, iters_done):
     tgt = O.TorchPolicy(cfg["hidden"], nf, a, cfg["log_std_init"])
     tgt.load_state_dict(beh.state_dict())
     roll_s = 0.0
-    if cfg.get("env") == "GridWorld":
+    if cfg.get("env") in ("GridWorld", "MountainCar"):
         # collect_particles (mepol.py:76-109): batch-1 policy.predict + env.step per step
         nsamp = 2
+        mc = cfg["env"] == "MountainCar"
+        if mc:
+            step, reset = O.mountaincar_step_scalar, lambda: np.array([rng.uniform(-0.6, -0.4), 0.0])
+        else:
+            step, reset = O.gridworld_step_scalar, lambda: rng.uniform(-6, -4, 2).astype(np.float32)
         t = time.perf_counter()
-        std = torch.exp(beh.log_std.detach())
-        for _ in range(nsamp):
-            s = rng.uniform(-6, -4, (1, 2)).astype(np.float32)
-            for _t in range(T):
-                with torch.no_grad():
-                    mu = beh.mean(beh.net(torch.as_tensor(s, dtype=torch.float64)))
-                    act = (mu + torch.randn(mu.shape, dtype=torch.float64) * std).numpy()
-                s = O.gridworld_step(s, act)
+        O.collect_particles_scalar(step, reset, beh, nsamp, T, nf, a)
         roll_s = (time.perf_counter() - t) * nt / nsamp
-        X = rng.uniform(-6, 6, (N, d)).astype(np.float32)
+        lo, hi = ((-1.2, 0.6) if mc else (-6, 6))
+        X = rng.uniform(lo, hi, (N, d)).astype(np.float32)
     else:
         X = rng.standard_normal((N, d)).astype(np.float32)
     nq = min(sample_queries, N)
@@ -454,9 +453,20 @@ def cpu_baseline(cfg, sample_queries, iters_done):
               f"(x{iters:g} + final H)")
     if roll_s:
         sample += f"; batch-1 rollout of 2 of {nt} trajectories x {T} steps (scaled) = {roll_s:.2f} s"
+    cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    ratio = None
+    if os.path.exists(cal):
+        try:
+            ratio = json.load(open(cal)).get("epoch_ratio_summary")
+        except Exception:
+            ratio = None
     return {"value": round(epoch_s, 3), "unit": "s/epoch", "cores": cores, "kind": "port",
             "sample": sample + "; torch f64 CPU", "cpu_model": _cpu_model(),
-            "affinity_cpus": aff}
+            "affinity_cpus": aff,
+            "components_s": {"rollout": round(roll_s, 3), "knn": round(knn_s, 3),
+                             "policy_update": round(upd_s, 3), "compute_kl": round(kl_s, 3),
+                             "iterations": iters},
+            "calibration_vs_reference": ratio}
 
 
 def main(argv=None):

@@ -266,10 +266,70 @@ class TorchPolicy(torch.nn.Module):
         self.mean = torch.nn.Linear(w[-1], a, dtype=torch.float64)
         self.log_std = torch.nn.Parameter(torch.full((a,), log_std_init, dtype=torch.float64))
 
+    def forward(self, x, deterministic=False):
+        """(mean, sample) as policy.py:53-61: the sample is drawn even when only the mean is
+        used (get_log_p), which is part of the reference's cost."""
+        mu = self.mean(self.net(x))
+        if deterministic:
+            return mu, mu
+        return mu, mu + torch.randn(mu.size(), dtype=torch.float64) * torch.exp(self.log_std)
+
+    def predict(self, s, deterministic=False):
+        """policy.py:64-67: batch-1 action for one state."""
+        with torch.no_grad():
+            x = torch.tensor(s, dtype=torch.float64).unsqueeze(0)
+            return self(x, deterministic=deterministic)[1][0]
+
     def get_log_p(self, s, a):
-        mu = self.mean(self.net(s))
+        mu, _ = self(s)
         return torch.sum(-0.5 * (math.log(2 * math.pi) + 2 * self.log_std
                                  + (a - mu) ** 2 / (torch.exp(self.log_std) + 1e-7) ** 2), dim=1)
+
+
+# Scalar (one env, one step) restatements of the env dynamics, in the reference's per-step shape:
+# the CPU baseline's rollout times these, as the reference steps one gym env per call.
+def gridworld_step_scalar(state, action, dim=6.0, max_delta=0.2):
+    """gridworld_continuous.py:128-154 for one env: f32 state [2], f64 action [2]."""
+    x, y = state
+    nx = x + np.clip(action[0], -max_delta, max_delta)
+    ny = y + np.clip(action[1], -max_delta, max_delta)
+    for (x0, x1, y0, y1) in GRID_WALLS:
+        if x0 <= nx <= x1 and y0 <= ny <= y1:
+            nx, ny = x, y
+    if np.abs(nx) >= dim or np.abs(ny) >= dim:
+        nx, ny = x, y
+    return np.array([nx, ny], dtype=np.float32)
+
+
+def mountaincar_step_scalar(state, action):
+    """mountain_car_wall.py:13-45 for one env: f64 state [2]."""
+    p, v = float(state[0]), float(state[1])
+    v += min(max(action[0], -1.0), 1.0) * 0.0015 - 0.0025 * math.cos(3 * p)
+    v = min(max(v, -0.07), 0.07)
+    p = min(max(p + v, -1.2), 0.6)
+    if p == -1.2 and v < 0:
+        v = 0.0
+    if p > 0.45:
+        p, v = 0.45, 0.0
+    return np.array([p, v])
+
+
+def collect_particles_scalar(step, reset, policy, num_traj, traj_len, nf, a_dim):
+    """collect_particles (mepol.py:70-111) in the reference's shape: for every trajectory and
+    step one batch-1 policy.predict and one scalar env step, recorded into f32 arrays, then the
+    next-state concatenation."""
+    states = np.zeros((num_traj, traj_len + 1, nf), dtype=np.float32)
+    actions = np.zeros((num_traj, traj_len, a_dim), dtype=np.float32)
+    for n in range(num_traj):
+        s = reset()
+        for t in range(traj_len):
+            states[n, t] = s
+            a = policy.predict(s).numpy()
+            actions[n, t] = a
+            s = step(s, a)
+        states[n, traj_len] = s
+    next_states = np.concatenate([states[n, 1:] for n in range(num_traj)], axis=0)
+    return states, actions, next_states
 
 
 def torch_iw(beh, tgt, states, actions, nt, lengths):
