@@ -13,8 +13,9 @@ build/%.o: mepol_amd/csrc/%.hip mepol_amd/csrc/common.hpp include/mepol_amd.h
 	@mkdir -p build
 	$(HIPCC) $(FLAGS) $(FLAGS_$*) -Iinclude -c $< -o $@
 
-# k-NN selection compares finite MFMA outputs: no NaN canonicalisation before v_min
-FLAGS_knn := -fno-honor-nans
+# k-NN selection compares finite MFMA outputs (inputs are validated first): no NaN
+# canonicalisation before v_min; MFMA results in VGPRs (no accvgpr copies per tile)
+FLAGS_knn := -fno-honor-nans -mllvm -amdgpu-mfma-vgpr-form
 
 $(LIB): $(OBJ)
 	$(HIPCC) $(FLAGS) -shared -o $@ $(OBJ)

@@ -104,10 +104,22 @@ __device__ __forceinline__ void list_insert(float (&ld)[LIST], int (&li)[LIST], 
 
 // Merge this lane's LDS buffer into its sorted list; then share the prune bound with the
 // partner lane (l ^ 32 serves the same query column).  Every lane of the wave calls it.
+// keep > 0 (split-f16 select): the bound also takes max(own keep-th, partner's keep-th): the
+// two half lists then hold >= 2 keep values at or below it, so 2 keep >= kp1 + slack of the
+// query's candidates in this range are never pruned; this bound is far tighter than a list's
+// own last entry (the LIST-th of one half).  The bound only decreases over the scan.
+template <int LIST>
+__device__ __forceinline__ float list_at(const float (&ld)[LIST], int j) {
+  float v = INFINITY;
+#pragma unroll
+  for (int i = 0; i < LIST; ++i) v = (i == j) ? ld[i] : v;
+  return v;
+}
+
 template <int LIST>
 __device__ __forceinline__ void flush_buffer(float (&ld)[LIST], int (&li)[LIST], float& thr, int& cnt,
                                              const float (*bv)[64], const int (*bi)[64], int l,
-                                             float thr0) {
+                                             float thr0, int keep = 0) {
   const int mc = wave_max_i(cnt);
 #pragma nounroll
   for (int e = 0; e < mc; ++e) {
@@ -122,9 +134,13 @@ __device__ __forceinline__ void flush_buffer(float (&ld)[LIST], int (&li)[LIST],
   }
   cnt = 0;
   // lanes l and l^32 serve the same query: the tighter of their maxima is a valid prune bound
-  // for both (refine's certification bound is the min over all partial-list maxima and the
+  // for both (refine's certification bound is the min over all lanes' final bounds and the
   // query's sampled bound thr0).
   thr = fminf(thr0, fminf(ld[LIST - 1], __shfl_xor(ld[LIST - 1], 32, kWave)));
+  if (keep > 0) {
+    const float kv = list_at<LIST>(ld, keep - 1);
+    thr = fminf(thr, fmaxf(kv, __shfl_xor(kv, 32, kWave)));
+  }
 }
 
 // Row (candidate within the tile) of accumulator register r for lane l (32x32 C/D map).
@@ -388,7 +404,8 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
                                                        const float* __restrict__ query,
                                                        int64_t nq, int d, int64_t nct, int split,
                                                        int64_t tiles_per_split, int tile_stride,
-                                                       int kp1, const unsigned* __restrict__ scal,
+                                                       int kp1, int keep,
+                                                       const unsigned* __restrict__ scal,
                                                        const float* __restrict__ tau_in,
                                                        float* __restrict__ tau_out,
                                                        float* __restrict__ out_v,
@@ -397,6 +414,7 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
   __shared__ int sbuf_i[4][kBufCap][64];
   const int w = threadIdx.x >> 6;
   const int l = threadIdx.x & 63;
+  if (TAU) keep = 0;
   // XCD-aware block mapping: workgroups go round-robin over the 8 XCDs by linear id, so with
   // sp = id % split (split a multiple of 8) every XCD only ever reads the candidate ranges
   // sp = xcd (mod 8), which then stay resident in that XCD's 4 MB L2 instead of streaming from
@@ -504,7 +522,8 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
           ++cnt;
         }
       }
-      if (__ballot(cnt > kBufCap - 16)) flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0);
+      if (__ballot(cnt > kBufCap - 16))
+        flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0, keep);
     }
   };
   if (t0 < t1) {
@@ -546,7 +565,7 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
       for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[b][v]));
     process(accP, t - 1);
   }
-  flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0);
+  flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0, keep);
 
   if (TAU) {
     // each half keeps its m = ceil(kp1/2) smallest; the union then holds 2m >= kp1 sampled
@@ -560,12 +579,19 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
     return;
   }
   if (qvalid) {
+    // The last slot carries this lane's final bound: every candidate of its range that is not
+    // in the list has an approximate value >= min(list last, thr) (rejected against thr, or
+    // evicted from the list); a last entry at or above the bound is dropped (idx -1), the
+    // bound covers it.  refine takes the min over the query's lanes.
+    const float bound = fminf(ld[LIST - 1], thr);
     const int64_t o = ((q * split + sp) * 2 + h) * LIST;
 #pragma unroll
-    for (int j = 0; j < LIST; ++j) {
+    for (int j = 0; j < LIST - 1; ++j) {
       out_v[o + j] = ld[j] * inv_s2;
       out_i[o + j] = li[j];
     }
+    out_v[o + LIST - 1] = bound * inv_s2;
+    out_i[o + LIST - 1] = (bound < ld[LIST - 1]) ? -1 : li[LIST - 1];
   }
 }
 
@@ -1011,6 +1037,8 @@ struct Plan {
   int sample;     // mode 1: tile stride of the sampling pass that seeds each query's bound (0: off)
   int filter;     // mode 1 + sampling: survivor filter pass (filter16_kernel) instead of lists
   int tau_list;   // list length of the sampling pass: >= ceil(kp1 / 2)
+  int keep;       // split-f16 lists: per-half entries behind the union prune bound (0: off)
+  int LIST16;     // split-f16 select: per-half list length (refine keeps LIST >= kp1 + 4)
   int M;          // refine input entries per query (lists: 2*split*LIST; filter: capacity)
   int list_len;   // refine: length of each ascending partial list (0: unsorted survivors)
   int64_t nc, nq, nct, nqt, tiles_per_split;
@@ -1018,7 +1046,7 @@ struct Plan {
 };
 
 static const int kKSChoices[] = {2, 4, 8, 12, 15, 16, 24, 32};
-static const int kListChoices[] = {8, 16, 40, 64};
+static const int kListChoices[] = {8, 16, 24, 32, 40, 64};
 
 static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Plan* P) {
   if (nc <= 0 || nq < 0 || d <= 0 || kp1 <= 0) {
@@ -1058,10 +1086,19 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
     const char* prec = getenv("MEPOL_KNN_PRECISION");
     const bool want_f32 = prec && (prec[0] == 'f' && prec[1] == '3' && prec[2] == '2');
     P->KS16 = (d + 1 + 15) / 16;
+    // split-f16 lists: each half-lane keeps LIST16 entries and prunes against the union bound
+    // (flush_buffer, keep = ceil(kp1/2) + 2 per half: 2 keep >= kp1 + 3).  A half holding more
+    // than LIST16 of the query's nearest candidates only costs certification (exact path).
+    P->keep = (kp1 + 1) / 2 + 2;
+    P->LIST16 = 64;
+    for (int v : kListChoices)
+      if (v >= P->keep + 4) {
+        P->LIST16 = v;
+        break;
+      }
     // split-f16 instantiations that stay below the 256-VGPR cap (at the cap the fragment
     // buffers of the asm-load pipeline are no longer safe from register copies)
-    const bool fits = P->KS16 == 1 || (P->KS16 == 2 && LIST <= 40) ||
-                      (P->KS16 == 3 && LIST <= 40);
+    const bool fits = P->LIST16 <= 40 && P->KS16 <= 3;
     P->mode = (!want_f32 && fits) ? 1 : 0;
     // f32: d + 1 fma-chain roundings, x4 margin.  split-f16: 3 K products per output summed in
     // f32 (<= 3K roundings), operand splitting 3 * 2^-22 = 12 * 2^-24, |c|^2 in f32 (d), x2.
@@ -1085,6 +1122,7 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   }
   P->KS = KS;
   P->KSP = (KS + 3) / 4 * 4;
+  if (P->mode != 1 || P->filter) P->keep = 0;
   P->LIST = LIST;
   P->nc = nc;
   P->nq = nq;
@@ -1113,8 +1151,9 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
     P->M = (int)align_up((size_t)std::max(256, std::min(cap, 2048)), 64);
     P->list_len = 0;
   } else {
-    P->M = 2 * split * LIST;
-    P->list_len = LIST;
+    const int sel_list = P->mode == 1 ? P->LIST16 : LIST;
+    P->M = 2 * split * sel_list;
+    P->list_len = sel_list;
   }
   P->maxp = (P->M + 63) / 64;
   if (P->maxp > 32) {
@@ -1156,6 +1195,14 @@ static void launch_select_ks(const Plan& P, dim3 g, const float* ap, const float
       hipLaunchKernelGGL((select_kernel<KS, KSP, 16>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
                          P.nct, P.split, P.tiles_per_split, lv, li);
       break;
+    case 24:
+      hipLaunchKernelGGL((select_kernel<KS, KSP, 24>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
+                         P.nct, P.split, P.tiles_per_split, lv, li);
+      break;
+    case 32:
+      hipLaunchKernelGGL((select_kernel<KS, KSP, 32>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
+                         P.nct, P.split, P.tiles_per_split, lv, li);
+      break;
     case 40:
       hipLaunchKernelGGL((select_kernel<KS, KSP, 40>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
                          P.nct, P.split, P.tiles_per_split, lv, li);
@@ -1174,22 +1221,30 @@ static void launch_select16_ks(const Plan& P, const _Float16* ap, const float* q
                                const unsigned* scal, float* tau, bool tau_pass, float* lv, int* li,
                                hipStream_t st) {
   const unsigned gx = (unsigned)((P.nqt + 3) / 4);
-#define MEPOL_SEL16(L)                                                                            \
-  if (tau_pass) {                                                                                 \
-    const int64_t ns = (P.nct + P.sample - 1) / P.sample;                                         \
-    hipLaunchKernelGGL((select16_kernel<KS16, L, true>), dim3(gx, 1), dim3(256), 0, st, ap, query, \
-                       P.nq, P.d, ns, 1, ns, P.sample, P.kp1, scal, nullptr, tau, nullptr,         \
-                       nullptr);                                                                  \
-  } else {                                                                                        \
-    hipLaunchKernelGGL((select16_kernel<KS16, L, false>), dim3(gx, (unsigned)P.split), dim3(256), \
-                       0, st, ap, query, P.nq, P.d, P.nct, P.split, P.tiles_per_split, 1, P.kp1,  \
-                       scal, tau, nullptr, lv, li);                                               \
+  if (tau_pass) {
+    const int64_t ns = (P.nct + P.sample - 1) / P.sample;
+#define MEPOL_TAU16(L)                                                                           \
+  hipLaunchKernelGGL((select16_kernel<KS16, L, true>), dim3(gx, 1), dim3(256), 0, st, ap, query, \
+                     P.nq, P.d, ns, 1, ns, P.sample, P.kp1, 0, scal, nullptr, tau, nullptr, nullptr)
+    switch (P.tau_list) {  // >= ceil(kp1 / 2), kp1 <= 60
+      case 8: MEPOL_TAU16(8); break;
+      case 16: MEPOL_TAU16(16); break;
+      case 24: MEPOL_TAU16(24); break;
+      default: MEPOL_TAU16(32); break;
+    }
+#undef MEPOL_TAU16
+    return;
   }
-  switch (tau_pass ? P.tau_list : P.LIST) {
+#define MEPOL_SEL16(L)                                                                            \
+  hipLaunchKernelGGL((select16_kernel<KS16, L, false>), dim3(gx, (unsigned)P.split), dim3(256), 0, \
+                     st, ap, query, P.nq, P.d, P.nct, P.split, P.tiles_per_split, 1, P.kp1, P.keep, \
+                     scal, tau, nullptr, lv, li)
+  switch (P.LIST16) {  // >= keep + 4 >= 7; mode 1 needs LIST16 <= 40
     case 8: MEPOL_SEL16(8); break;
     case 16: MEPOL_SEL16(16); break;
-    case 40: MEPOL_SEL16(40); break;
-    default: MEPOL_SEL16(64); break;
+    case 24: MEPOL_SEL16(24); break;
+    case 32: MEPOL_SEL16(32); break;
+    default: MEPOL_SEL16(40); break;
   }
 #undef MEPOL_SEL16
 }
@@ -1322,18 +1377,16 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
         switch (P.KS16) {
           case 1: MEPOL_FLT16(1); break;
           case 2: MEPOL_FLT16(2); break;
-          case 3: MEPOL_FLT16(3); break;
-          default: MEPOL_FLT16(4); break;
+          default: MEPOL_FLT16(3); break;
         }
 #undef MEPOL_FLT16
         MEPOL_CHECK_LAUNCH();
         continue;
       }
-      switch (P.KS16) {
+      switch (P.KS16) {  // mode 1 only for KS16 <= 3 (make_plan)
         case 1: launch_select16_ks<1>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
         case 2: launch_select16_ks<2>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
-        case 3: launch_select16_ks<3>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
-        default: launch_select16_ks<4>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
+        default: launch_select16_ks<3>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
       }
       MEPOL_CHECK_LAUNCH();
     }
@@ -1358,6 +1411,8 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
   switch (P.LIST) {
     case 8: launch_refine_list<8>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
     case 16: launch_refine_list<16>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
+    case 24: launch_refine_list<24>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
+    case 32: launch_refine_list<32>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
     case 40: launch_refine_list<40>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
     default: launch_refine_list<64>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
   }
@@ -1366,6 +1421,8 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
   switch (P.LIST) {
     case 8: launch_exact_list<8>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
     case 16: launch_exact_list<16>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
+    case 24: launch_exact_list<24>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
+    case 32: launch_exact_list<32>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
     case 40: launch_exact_list<40>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
     default: launch_exact_list<64>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
   }
