@@ -124,6 +124,9 @@ class DeviceIteration:
         self.ws_layer = ops.layer_workspace(self.N, W1.shape[1], W1.shape[0], dev)
         self.graph = None
         self.fork = torch.cuda.Stream(device=dev)
+        self.s_gemm = torch.cuda.Stream(device=dev)
+        self.s_head = torch.cuda.Stream(device=dev)
+        self.ranges = _row_chunks(self.N)
         self._batch_id = None
         self._init_state()
 
@@ -198,13 +201,75 @@ class DeviceIteration:
 
     @torch.no_grad()
     def forward(self):
-        """logp of the target at its current parameters into the static buffers."""
+        """logp of the target at its current parameters into the static buffers.
+
+        Row chunks are software-pipelined over three streams: layer 1 of chunk c+1 (HBM-bound,
+        current stream) and the head of chunk c-1 (HBM-bound, s_head) run while the f64 GEMM of
+        chunk c (MFMA-bound, s_gemm) does."""
         W1, b1, W2, b2, Wm, bm, ls = self.named
-        ops.layer_forward(self.x, W1, b1, out=self.h1)
-        torch.mm(self.h1, W2.t(), out=self.z2)
-        ops.head_forward(self.z2, Wm, bm, ls, self.act, bz=b2, mu_out=self.mu, logp_out=self.logp)
+        if len(self.ranges) == 1:
+            ops.layer_forward(self.x, W1, b1, out=self.h1)
+            torch.mm(self.h1, W2.t(), out=self.z2)
+            ops.head_forward(self.z2, Wm, bm, ls, self.act, bz=b2, mu_out=self.mu,
+                             logp_out=self.logp)
+            return
+        cur = torch.cuda.current_stream()
+        self.s_gemm.wait_stream(cur)
+        self.s_head.wait_stream(cur)
+        for r0, r1 in self.ranges:
+            ops.layer_forward(self.x[r0:r1], W1, b1, out=self.h1[r0:r1])
+            e_l = torch.cuda.Event()
+            e_l.record(cur)
+            self.s_gemm.wait_event(e_l)
+            with torch.cuda.stream(self.s_gemm):
+                torch.mm(self.h1[r0:r1], W2.t(), out=self.z2[r0:r1])
+                e_g = torch.cuda.Event()
+                e_g.record(self.s_gemm)
+            self.s_head.wait_event(e_g)
+            with torch.cuda.stream(self.s_head):
+                ops.head_forward(self.z2[r0:r1], Wm, bm, ls, self.act[r0:r1], bz=b2,
+                                 mu_out=self.mu[r0:r1], logp_out=self.logp[r0:r1])
+        cur.wait_stream(self.s_gemm)
+        cur.wait_stream(self.s_head)
 
     refresh = forward
+
+    def _backward(self, grad):
+        """(dW1, db1, dW2, db2, dWm, dbm, dls) from dH/dlogp: the _TwoLayerLogp backward.
+
+        One chunk: head backward, then dW2 (split-K GEMM, forked stream) concurrent with
+        dh1 -> layer-1 backward.  Several chunks: the head backward of chunk c+1 (HBM-bound)
+        also overlaps the GEMMs of chunk c; per-chunk weight gradients are summed in chunk
+        order (fixed, so the result is reproducible)."""
+        W1, b1, W2, b2, Wm, bm, ls = self.named
+        cur = torch.cuda.current_stream()
+        self.fork.wait_stream(cur)
+        self.s_gemm.wait_stream(cur)
+        parts, keep = [], []
+        for r0, r1 in self.ranges:
+            sl = slice(r0, r1)
+            dz2, dWm, dbm, dls, db2 = ops.head_backward(grad[sl], self.z2[sl], Wm, ls,
+                                                        self.act[sl], self.mu[sl], bz=b2,
+                                                        need_dz=True, ws=self.ws_head)
+            e_h = torch.cuda.Event()
+            e_h.record(cur)
+            # dW2 (split-K GEMM) on a forked stream, concurrent with dh1 -> layer-1 backward:
+            # the memory-bound layer kernel overlaps the MFMA-bound GEMM.
+            self.fork.wait_event(e_h)
+            with torch.cuda.stream(self.fork):
+                dW2 = _weight_grad(dz2, self.h1[sl])
+            self.s_gemm.wait_event(e_h)
+            with torch.cuda.stream(self.s_gemm):
+                dh1 = torch.mm(dz2, W2)
+                dW1, db1 = ops.layer_backward(dh1, self.h1[sl], self.x[sl], ws=self.ws_layer)
+            keep += [dz2, dh1]
+            parts.append((dW1, db1, dW2, db2, dWm, dbm, dls))
+        cur.wait_stream(self.fork)
+        cur.wait_stream(self.s_gemm)
+        del keep
+        if len(parts) == 1:
+            return parts[0]
+        return tuple(torch.stack([p[i] for p in parts]).sum(0) for i in range(7))
 
     @torch.no_grad()
     def _body(self):
@@ -219,17 +284,7 @@ class DeviceIteration:
         grad = ops.entropy_reverse_scan(gamma, w, partials, nparts, self.offsets, nt, T,
                                         self.neg_one)
         # through the policy (the _TwoLayerLogp backward)
-        dz2, dWm, dbm, dls, db2 = ops.head_backward(grad.view(-1), self.z2, Wm, ls, self.act,
-                                                    self.mu, bz=b2, need_dz=True, ws=self.ws_head)
-        # dW2 (split-K GEMM) on a forked stream, concurrent with dh1 -> layer-1 backward: the
-        # memory-bound layer kernel overlaps the MFMA-bound GEMM.
-        cur = torch.cuda.current_stream()
-        self.fork.wait_stream(cur)
-        with torch.cuda.stream(self.fork):
-            dW2 = _weight_grad(dz2, self.h1)
-        dh1 = torch.mm(dz2, W2)
-        dW1, db1 = ops.layer_backward(dh1, self.h1, self.x, ws=self.ws_layer)
-        cur.wait_stream(self.fork)
+        dW1, db1, dW2, db2, dWm, dbm, dls = self._backward(grad.view(-1))
         # optimizer.step() (mepol.py:280)
         grad_of = {id(p): g for p, g in zip(self.named, (dW1, db1, dW2, db2, dWm, dbm, dls))}
         ops.optim_step(self.kind, self.params, [grad_of[id(p)] for p in self.params], self.m,
@@ -275,6 +330,16 @@ class DeviceIteration:
         self.graph.replay()
         v = self.vals.cpu()
         return float(v[0]), float(v[1])
+
+
+def _row_chunks(n):
+    """Row ranges of the pipelined forward/backward: MEPOL_ITER_CHUNKS (default 1) chunks of
+    at least 32768 rows (64-row aligned), one chunk for smaller batches."""
+    want = int(os.environ.get("MEPOL_ITER_CHUNKS", "1"))
+    c = max(1, min(want, n // 32768))
+    step = -(-n // c)
+    step = -(-step // 64) * 64
+    return [(r, min(n, r + step)) for r in range(0, n, step)]
 
 
 _CACHE = weakref.WeakKeyDictionary()  # target policy -> DeviceIteration

@@ -1135,9 +1135,14 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
     split = 8;
     while (split > 1 && P->nct / split < 16) split >>= 1;
   } else if (split <= 0) {
-    // enough waves to fill 256 CUs x ~3 waves/SIMD several times over, tiles >= 16 per split
-    const int64_t target = 16384;
+    // enough waves to fill 256 CUs x 2 waves/SIMD several times over, tiles >= 16 per split.
+    // Every (query, split) pays the list warm-up (the prune bound starts at +inf), so fewer,
+    // longer ranges win once the chip is full: C3 split 2 = 12.9 ms, 3 = 13.4, 8 = 17.2
+    // (tools/knn_splits.sh).  The split-f16 lists keep >= 2 ranges (one range of 24-entry half
+    // lists certifies too few queries).
+    const int64_t target = P->mode == 1 ? 12500 : 16384;
     split = (int)std::min<int64_t>(kMaxSplit, std::max<int64_t>(1, (target + P->nqt - 1) / std::max<int64_t>(P->nqt, 1)));
+    if (P->mode == 1) split = std::max(split, 2);
     while (split > 1 && P->nct / split < 16) --split;
   }
   split = std::max(1, std::min(split, kMaxSplit));

@@ -27,7 +27,6 @@ import torch
 
 from . import ops as _hip_ops
 from .algorithms.device_loop import DeviceIteration
-from .policy import _weight_grad
 
 
 class ShardedEpoch:
@@ -307,11 +306,7 @@ class ShardedIteration(DeviceIteration):
         S = ep._sum(partials[:nparts].sum().reshape(1)).reshape(())
         grad = ops.entropy_reverse_scan(gamma, w_local, partials, nparts, self.offsets, nt, T,
                                         self.neg_one, S_ext=S)
-        dz2, dWm, dbm, dls, db2 = ops.head_backward(grad.view(-1), self.z2, Wm, ls, self.act,
-                                                    self.mu, bz=b2, need_dz=True, ws=self.ws_head)
-        dW2 = _weight_grad(dz2, self.h1)
-        dh1 = torch.mm(dz2, W2)
-        dW1, db1 = ops.layer_backward(dh1, self.h1, self.x, ws=self.ws_layer)
+        dW1, db1, dW2, db2, dWm, dbm, dls = self._backward(grad.view(-1))
         grad_of = {id(p): t for p, t in zip(self.named, (dW1, db1, dW2, db2, dWm, dbm, dls))}
         flat = torch.cat([grad_of[id(p)].reshape(-1) for p in self.params])
         self.dist.all_reduce(flat, group=self.group)  # ShardedEpoch.allreduce_grads

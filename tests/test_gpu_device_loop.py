@@ -16,6 +16,8 @@ SMALL = dict(NT=NT, T=T, NF=NF, A=A, K=K, HID=HID)
 C3 = dict(NT=40, T=500, NF=29, A=8, K=30, HID=[400, 300])
 C4 = dict(NT=40, T=500, NF=47, A=17, K=30, HID=[400, 300])
 C5 = dict(NT=400, T=50, NF=63, A=20, K=50, HID=[400, 300])
+# large enough for the 4-chunk pipelined forward/backward (algorithms/device_loop._row_chunks)
+BIG = dict(NT=256, T=512, NF=29, A=8, K=10, HID=[64, 48])
 
 
 def _setup(opt_name, lr, seed=5, cfg=None):
@@ -70,8 +72,11 @@ def _run(monkeypatch, graph, opt_name, lr, kl_threshold, max_off_iters=6, cfg=No
     ("adam", 5e-2, 1e-3, SMALL),     # early rejection -> backtracking with halved lr
     ("rmsprop", 1e-4, 10.0, SMALL),
     ("adam", 1e-4, 10.0, C4),        # wide action head (a = 17)
+    ("adam", 1e-3, 10.0, BIG),       # 4 row chunks pipelined over three streams
 ])
 def test_graph_loop_matches_eager(cuda, monkeypatch, opt_name, lr, kl_threshold, cfg):
+    if cfg is BIG:  # the row-chunk pipeline is off by default (measured slower at C3)
+        monkeypatch.setenv("MEPOL_ITER_CHUNKS", "4")
     g = _run(monkeypatch, True, opt_name, lr, kl_threshold, cfg=cfg)
     e = _run(monkeypatch, False, opt_name, lr, kl_threshold, cfg=cfg)
     assert g["used"] and not e["used"]
@@ -153,3 +158,15 @@ def test_graph_scratch_survives_eager_growth(cuda, monkeypatch):
     e_out, e_params = _two_epochs(monkeypatch, False)
     np.testing.assert_allclose(g_out, e_out, rtol=1e-9)
     np.testing.assert_allclose(g_params, e_params, rtol=1e-8, atol=1e-11)
+
+
+def test_row_chunks_cover_the_batch():
+    from mepol_amd.algorithms.device_loop import _row_chunks
+
+    for n in (1, 20000, 65535, 131072, 200000, 500000):
+        r = _row_chunks(n)
+        assert r[0][0] == 0 and r[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+        assert all(r1 > r0 for r0, r1 in r)
+        assert all(r0 % 64 == 0 for r0, _ in r)
+    assert len(_row_chunks(20000)) == 1
