@@ -331,12 +331,13 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
 
 // Backward for wide action spaces (8 < A <= 32: Humanoid 17, HandReach 20).  The per-lane dWm
 // accumulators of head_bwd_kernel would be NC x A doubles (5 x 24 at H = 300: over the register
-// file), so here the block's 256 lanes split the columns of one row (c = tid + 256 j, j < NC)
-// and every wave accumulates NC x AP values.  dmu is lane-distributed (lane a holds component a)
-// and broadcast with v_readlane; Wm sits in LDS as [a][Hs] (Hs = H rounded up to 64, dynamic
-// LDS, AP * Hs doubles).  The block walks rows i = blockIdx.x, += gridDim.x (fixed order), so
-// each block's partial record [dW (A*H) | db (A) | dls (A) | dbz (H)] is deterministic and
-// reduce_partials_kernel sums the records in a fixed order as for head_bwd_kernel.
+// file), so here a block of ceil(H/64) waves owns one column per lane (c = threadIdx.x) and each
+// lane accumulates AP values.  kRows rows per step share each Wm read from LDS and give the FMA
+// chains independent work.  dmu is lane-distributed (lane a holds component a) and broadcast with
+// v_readlane; Wm sits in LDS as [a][Hs] (Hs = block width, dynamic LDS, AP * Hs doubles).  The
+// block walks rows in a fixed order (grid-stride), so each block's partial record
+// [dW (A*H) | db (A) | dls (A) | dbz (H)] is deterministic and reduce_partials_kernel sums the
+// records in a fixed order as for head_bwd_kernel.
 __device__ __forceinline__ double readlane_d(double v, int lane) {
   const long long b = __double_as_longlong(v);
   const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), lane);
@@ -344,14 +345,16 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-template <int AP, int NC>
-__global__ __launch_bounds__(256) void head_bwd_wide_kernel(
+template <int AP>
+__global__ __launch_bounds__(512) void head_bwd_wide_kernel(
     const double* __restrict__ gl, const double* __restrict__ z, int64_t N, int H, int Hs,
     const double* __restrict__ bz, const double* __restrict__ Wm, const double* __restrict__ log_std,
     const double* __restrict__ act, const double* __restrict__ mu, int A,
     double* __restrict__ dz, double* __restrict__ part) {
-  extern __shared__ double sWd[];  // [a < AP][c < Hs]
+  constexpr int kRows = 2;
+  extern __shared__ double sWd[];  // [a < AP][c < Hs], then dmu[wave][row][a < AP]
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  double2* sDm = reinterpret_cast<double2*>(sWd + AP * Hs) + w * (kRows * AP / 2);
   for (int e = tid; e < AP * Hs; e += blockDim.x) {
     const int a = e / Hs, c = e % Hs;
     sWd[e] = (a < A && c < H) ? Wm[a * H + c] : 0.0;
@@ -364,80 +367,86 @@ __global__ __launch_bounds__(256) void head_bwd_wide_kernel(
     es3 = e / (sd * sd * sd);
   }
   __syncthreads();
-  // wave-uniform: does this wave own any valid column in slot j?
-  bool live[NC];
-  double bzr[NC], accz[NC], accW[NC][AP];
+  const int c = tid;
+  const int cc = c < H ? c : H - 1;  // clamped column: loads in bounds, results discarded
+  const double bzc = (bz && c < H) ? bz[c] : 0.0;
+  double accW[AP];
 #pragma unroll
-  for (int j = 0; j < NC; ++j) {
-    live[j] = (w * 64 + 256 * j) < H;
-    const int c = tid + 256 * j;
-    bzr[j] = (bz && c < H) ? bz[c] : 0.0;
-    accz[j] = 0.0;
-#pragma unroll
-    for (int a = 0; a < AP; ++a) accW[j][a] = 0.0;
-  }
-  double accb = 0.0, accls = 0.0;
+  for (int a = 0; a < AP; ++a) accW[a] = 0.0;
+  double accz = 0.0, accb = 0.0, accls = 0.0;
   const int64_t last = N - 1;
   const int la = l < A ? l : A - 1;
   struct Slot {
-    double z[NC];
-    double g, av, mv;
+    double z[kRows], g[kRows], av[kRows], mv[kRows];
   };
   auto load_slot = [&](Slot& s, int64_t i) {
-    const int64_t ic = i < N ? i : last;
-    const double* zr = z + ic * H;
 #pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      const int c = tid + 256 * j;
-      s.z[j] = zr[c < H ? c : H - 1];
+    for (int r = 0; r < kRows; ++r) {
+      const int64_t ic = i + r < N ? i + r : last;
+      s.z[r] = z[ic * H + cc];
+      s.g[r] = gl[ic];
+      s.av[r] = act[ic * A + la];
+      s.mv[r] = mu[ic * A + la];
     }
-    s.g = gl[ic];
-    s.av = act[ic * A + la];
-    s.mv = mu[ic * A + la];
   };
+  const int64_t stride = (int64_t)gridDim.x * kRows;
+  const int64_t i0 = (int64_t)__builtin_amdgcn_readfirstlane((int)blockIdx.x) * kRows;
   Slot cur;
-  const int64_t i0 = __builtin_amdgcn_readfirstlane((int)blockIdx.x);
   load_slot(cur, i0);
-  for (int64_t i = i0; i < N; i += gridDim.x) {
+  for (int64_t i = i0; i < N; i += stride) {
     Slot s = cur;
-    load_slot(cur, i + gridDim.x);
-    const double d = (l < A) ? s.av - s.mv : 0.0;
-    const double dm = s.g * d * inv;  // 0 for lanes >= A
-    if (l < A) {
-      accb += dm;
-      accls += s.g * (-1.0 + d * d * es3);
+    load_slot(cur, i + stride);
+    double dm[kRows], x[kRows], zb[kRows], dh[kRows];
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const bool rowv = i + r < N;
+      const double d = (l < A && rowv) ? s.av[r] - s.mv[r] : 0.0;
+      dm[r] = s.g[r] * d * inv;  // 0 for lanes >= A and rows past N
+      if (l < A && rowv) {
+        accb += dm[r];
+        accls += s.g[r] * (-1.0 + d * d * es3);
+      }
+      zb[r] = s.z[r] + bzc;
+      x[r] = rowv ? fmax(zb[r], 0.0) : 0.0;
+      dh[r] = 0.0;
     }
-    int cl = tid;
+    // broadcast dmu through this wave's LDS slot (one wave's LDS ops complete in order):
+    // lane a writes component a, every lane reads pairs with ds_read_b128
+    if (l < AP) {
+#pragma unroll
+      for (int r = 0; r < kRows; ++r) reinterpret_cast<double*>(sDm)[r * AP + l] = dm[r];
+    }
+    int cl = c;
     asm volatile("" : "+v"(cl));  // keep the Wm LDS reads in the loop
 #pragma unroll
-    for (int j = 0; j < NC; ++j) {
-      if (!live[j]) continue;
-      const int c = tid + 256 * j;
-      const double zb = s.z[j] + bzr[j];
-      const double x = fmax(zb, 0.0);
-      double dh = 0.0;
+    for (int a2 = 0; a2 < AP / 2; ++a2) {
+      const double w0 = sWd[(2 * a2) * Hs + cl];
+      const double w1 = sWd[(2 * a2 + 1) * Hs + cl];
 #pragma unroll
-      for (int a = 0; a < AP; ++a) {
-        const double sa = readlane_d(dm, a);
-        dh = fma(sa, sWd[a * Hs + cl + 256 * j], dh);
-        accW[j][a] = fma(sa, x, accW[j][a]);
+      for (int r = 0; r < kRows; ++r) {
+        const double2 sa = sDm[r * (AP / 2) + a2];
+        dh[r] = fma(sa.x, w0, dh[r]);
+        dh[r] = fma(sa.y, w1, dh[r]);
+        accW[2 * a2] = fma(sa.x, x[r], accW[2 * a2]);
+        accW[2 * a2 + 1] = fma(sa.y, x[r], accW[2 * a2 + 1]);
       }
-      const double dzv = (zb > 0.0) ? dh : 0.0;
-      accz[j] += dzv;
-      if (dz && c < H) dz[i * H + c] = dzv;
+    }
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) {
+      const double dzv = (zb[r] > 0.0) ? dh[r] : 0.0;
+      if (i + r < N) {
+        accz += dzv;
+        if (dz && c < H) dz[(i + r) * H + c] = dzv;
+      }
     }
   }
   const int64_t m = (int64_t)A * H + 2 * A + H;
   double* rec = part + (int64_t)blockIdx.x * m;
+  if (c < H) {
 #pragma unroll
-  for (int j = 0; j < NC; ++j) {
-    const int c = tid + 256 * j;
-    if (c < H) {
-#pragma unroll
-      for (int a = 0; a < AP; ++a)
-        if (a < A) rec[a * H + c] = accW[j][a];
-      rec[A * H + 2 * A + c] = accz[j];
-    }
+    for (int a = 0; a < AP; ++a)
+      if (a < A) rec[a * H + c] = accW[a];
+    rec[A * H + 2 * A + c] = accz;
   }
   // db / dlog_std: every wave accumulated the same rows' components; wave 0 writes
   if (w == 0 && l < A) {
@@ -551,23 +560,22 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
   hipStream_t st = (hipStream_t)stream;
   double* pdW = (double*)workspace;
   if (a_dim > 8) {
-    const int apw = a_dim <= 16 ? 16 : a_dim <= 24 ? 24 : 32;
-    const int ncw = (hidden + 255) / 256;
-    const int hs = (hidden + 63) / 64 * 64;
-    const size_t lds = (size_t)apw * hs * sizeof(double);
-#define MEPOL_HEAD_BWDW(AP_, NC_)                                                               \
-  if (apw == AP_ && ncw == NC_) {                                                               \
+    const int apw = a_dim <= 12 ? 12 : a_dim <= 16 ? 16 : a_dim <= 20 ? 20 : a_dim <= 24 ? 24 : 32;
+    const int hs = (hidden + 63) / 64 * 64;  // block width: one column per lane
+    const size_t lds = ((size_t)apw * hs + (size_t)(hs / 64) * 2 * apw) * sizeof(double);
+#define MEPOL_HEAD_BWDW(AP_)                                                                    \
+  if (apw == AP_) {                                                                             \
     static bool attr_set = false;                                                               \
     if (!attr_set) {                                                                            \
-      MEPOL_HIP(hipFuncSetAttribute((const void*)head_bwd_wide_kernel<AP_, NC_>,                \
+      MEPOL_HIP(hipFuncSetAttribute((const void*)head_bwd_wide_kernel<AP_>,                     \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));   \
       attr_set = true;                                                                          \
     }                                                                                           \
-    hipLaunchKernelGGL((head_bwd_wide_kernel<AP_, NC_>), dim3(nb), dim3(256), lds, st, grad_logp, \
-                       z, n, hidden, hs, bz, Wm, log_std, act, mu, a_dim, dz, pdW);             \
+    hipLaunchKernelGGL((head_bwd_wide_kernel<AP_>), dim3(nb), dim3(hs), lds, st, grad_logp, z, n, \
+                       hidden, hs, bz, Wm, log_std, act, mu, a_dim, dz, pdW);                   \
   }
-    MEPOL_HEAD_BWDW(16, 1) MEPOL_HEAD_BWDW(16, 2) MEPOL_HEAD_BWDW(24, 1) MEPOL_HEAD_BWDW(24, 2)
-    MEPOL_HEAD_BWDW(32, 1) MEPOL_HEAD_BWDW(32, 2)
+    MEPOL_HEAD_BWDW(12) MEPOL_HEAD_BWDW(16) MEPOL_HEAD_BWDW(20) MEPOL_HEAD_BWDW(24)
+    MEPOL_HEAD_BWDW(32)
 #undef MEPOL_HEAD_BWDW
     MEPOL_CHECK_LAUNCH();
     const int64_t m = (int64_t)a_dim * hidden + 2 * a_dim + hidden;
