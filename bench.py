@@ -174,6 +174,9 @@ def run(args):
         os.environ.setdefault("WORLD_SIZE", str(world))
         backend = os.environ.get("MEPOL_BENCH_BACKEND", "nccl")  # nccl == RCCL on ROCm
         if backend == "nccl":
+            from mepol_amd.parallel import prepare_nccl_env
+
+            prepare_nccl_env()
             dist.init_process_group("nccl", device_id=dev)
         else:  # rehearsal: several ranks share one GPU over gloo
             dist.init_process_group(backend)

@@ -129,6 +129,9 @@ def main(argv=None):
         torch.cuda.set_device(local)
         if not dist.is_initialized():
             if ndev >= world:
+                from ..parallel import prepare_nccl_env
+
+                prepare_nccl_env()
                 dist.init_process_group("nccl", device_id=torch.device("cuda", local))
             else:
                 dist.init_process_group("gloo")

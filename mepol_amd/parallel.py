@@ -21,12 +21,22 @@ so every rank holds the same H, KL and parameters and takes the same accept/back
 The kernels come from `ops` (the HIP library).  Tests may inject another object with the same
 functions to check this module's collective algebra on CPU with the gloo backend.
 """
+import os
 import weakref
 
 import torch
 
 from . import ops as _hip_ops
 from .algorithms.device_loop import DeviceIteration
+
+
+def prepare_nccl_env():
+    """Call before init_process_group("nccl") in a process that captures collectives
+    (ShardedIteration.try_capture).  ProcessGroupNCCL recycles the HIP events of finished works
+    (TORCH_NCCL_CUDA_EVENT_CACHE); an event last recorded inside a graph capture can then reach
+    the watchdog thread, whose query fails with hipErrorCapturedEvent and aborts the process.
+    Without the cache every work gets fresh events.  A caller's explicit setting wins."""
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
 class ShardedEpoch:
@@ -335,7 +345,10 @@ class ShardedIteration(DeviceIteration):
         ok = 1
         try:
             self._capture_graph()
-        except Exception:  # capture unsupported here: every rank falls back together
+        except Exception as e:  # capture unsupported here: every rank falls back together
+            import warnings
+
+            warnings.warn(f"sharded iteration capture failed, running eagerly: {e!r}")
             self.graph = None
             ok = 0
             torch.cuda.synchronize()

@@ -32,6 +32,9 @@ def nccl_world1():
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(_port())
     torch.cuda.set_device(0)
+    from mepol_amd.parallel import prepare_nccl_env
+
+    prepare_nccl_env()
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
     yield dist
     dist.destroy_process_group()
