@@ -129,6 +129,28 @@ int mepol_layer_backward(const double* dh, const double* h, const double* x, int
                          int in_features, int out_features, double* dW, double* db,
                          void* workspace, size_t workspace_bytes, void* stream);
 
+/* Fused policy forward for the large-batch passes (GaussianPolicy.get_log_p, src/policy.py:21-51,
+ * net = Linear(nf,h0) ReLU Linear(h0,h1) ReLU, mean = Linear(h1,a)): h1 = relu(x W1^T + b1)
+ * [n, h0], z2 = h1 W2^T [n, h1] (pre-bias, as the head kernels take it), mu [n, a] and logp [n]
+ * in one kernel.  in_features <= 64, hidden1 <= 320; W2 16-byte aligned. */
+int mepol_policy_forward(const double* x, int64_t n, int in_features, const double* W1,
+                         const double* b1, int hidden0, const double* W2, const double* b2,
+                         int hidden1, const double* Wm, const double* bm, const double* log_std,
+                         const double* actions, int action_dim, double* h1_out, double* z2_out,
+                         double* mu_out, double* logp_out, void* stream);
+
+/* Hidden layer on the f64 matrix cores: C = act(A B^T + bias), A [n, k] (row stride lda),
+ * B [m, k] (ldb), bias [m] (nullable), C [n, m] (ldc); act = ReLU when relu != 0.  k, lda, ldb
+ * even and A, B 16-byte aligned.  variant 0 = default tiling.  Replaces the torch.mm /
+ * nn.Linear GEMMs of GaussianPolicy.net (src/policy.py:21-26) in the large-batch passes. */
+int mepol_gemm_nt(const double* A, int64_t n, int k, int64_t lda, const double* B, int m,
+                  int64_t ldb, const double* bias, int relu, double* C, int64_t ldc, int variant,
+                  void* stream);
+/* Tuning experiment: the same product on the VALU (v_fmac_f64 with DPP row broadcast). */
+int mepol_gemm_dpp(const double* A, int64_t n, int k, int64_t lda, const double* B, int m,
+                   int64_t ldb, const double* bias, int relu, double* C, int64_t ldc, int variant,
+                   void* stream);
+
 /* ---- environments -------------------------------------------------------------------------
  * Replace MountainCarContinuous.step (src/envs/mountain_car_wall.py:13-45) and
  * GridWorldContinuous.step (src/envs/gridworld_continuous.py:128-154), batched. */

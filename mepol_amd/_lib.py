@@ -48,6 +48,13 @@ SIGNATURES = {
     "mepol_layer_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
     "mepol_layer_backward": [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_sz,
                              _c_vp],
+    "mepol_policy_forward": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
+                             _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
+                             _c_vp],
+    "mepol_gemm_nt": [_c_vp, _c_i64, _c_int, _c_i64, _c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_vp,
+                      _c_i64, _c_int, _c_vp],
+    "mepol_gemm_dpp": [_c_vp, _c_i64, _c_int, _c_i64, _c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_vp,
+                       _c_i64, _c_int, _c_vp],
     "mepol_step_mountaincar": [_c_vp, _c_vp, _c_i64, _c_i64, _c_vp],
     "mepol_step_gridworld": [_c_vp, _c_vp, _c_i64, _c_vp],
     "mepol_rollout_step": [_c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_i64,

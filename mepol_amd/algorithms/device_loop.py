@@ -114,6 +114,8 @@ class DeviceIteration:
         self.z2 = torch.empty((self.N, W2.shape[0]), **f64)
         self.mu = torch.empty((self.N, Wm.shape[0]), **f64)
         self.logp = torch.empty(self.N, **f64)
+        self.fused_fwd = (ops.policy_forward_ok(self.x.shape[1], W2.shape[0])
+                          and os.environ.get("MEPOL_FUSED_FWD", "1") != "0")
         self.neg_one = torch.full((), -1.0, **f64)
         self.scal = torch.zeros(8, **f64)
         self.scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
@@ -207,6 +209,12 @@ class DeviceIteration:
         current stream) and the head of chunk c-1 (HBM-bound, s_head) run while the f64 GEMM of
         chunk c (MFMA-bound, s_gemm) does."""
         W1, b1, W2, b2, Wm, bm, ls = self.named
+        if self.fused_fwd:  # layer 1 + z2 GEMM + head in one kernel per row chunk
+            for r0, r1 in self.ranges:
+                ops.policy_forward(self.x[r0:r1], W1, b1, W2, b2, Wm, bm, ls, self.act[r0:r1],
+                                   self.h1[r0:r1], self.z2[r0:r1], self.mu[r0:r1],
+                                   self.logp[r0:r1])
+            return
         if len(self.ranges) == 1:
             ops.layer_forward(self.x, W1, b1, out=self.h1)
             torch.mm(self.h1, W2.t(), out=self.z2)

@@ -1,0 +1,333 @@
+// Fused forward of GaussianPolicy.get_log_p for the large-batch off-policy passes
+// (src/policy.py:21-51: net = Linear(nf, h0) ReLU Linear(h0, h1) ReLU, mean = Linear(h1, a),
+// logp = sum_a log N(act | mean, exp(log_std) + 1e-7)) as ONE kernel per 64-row block:
+//
+//   h1 = relu(x W1^T + b1)      f64 MFMA, K = nf (<= 64), a k-tile of h1 at a time, written to
+//                               LDS as the next GEMM's A operand and to HBM (h1_out: the
+//                               backward's dW2 operand and ReLU mask)
+//   z2 = h1 W2^T                f64 MFMA (v_mfma_f64_16x16x4f64), 64 x 320 output tile per
+//                               workgroup (8 waves, 32 x 80 each), K = h0 streamed in 16-tiles
+//                               through double-buffered LDS; z2 (pre-bias) written to HBM for
+//                               the head backward
+//   mu = relu(z2 + b2) Wm^T + bm, logp   epilogue on the accumulators: per-lane partial mean
+//                               over the lane's 5 columns, reduce-scatter over the 16 lanes of a
+//                               row, fixed-order sum of the 4 column waves through LDS
+//
+// This replaces layer_forward + the z2 GEMM + head_forward (three passes over the N x h0 and
+// N x h1 activations) with one: the layer-1 recompute costs ceil4(nf)/320 of the GEMM's MFMA
+// work (10 % at nf = 29) and the head epilogue ~2 %.  Limits: nf <= 64, h1 (hidden[1]) <= 320.
+#include "common.hpp"
+
+namespace mepol {
+namespace pfwd {
+
+constexpr int BM = 64, BN = 320;     // output tile (rows x h1 columns)
+constexpr int WC = 4;                // column waves (80 columns each); 2 row waves (32 rows)
+constexpr int FR = 2, FC = 5;        // 16x16 fragments per wave
+constexpr int kThreads = 512;
+constexpr int KT = 16, KP = 18;      // k-tile and padded LDS row (doubles)
+constexpr int CB = BN * (KT / 2), PB = CB / kThreads;  // 16-B chunks of a W2 k-tile per thread
+constexpr int kAChunk = 8;           // actions per epilogue pass
+constexpr double kLog2Pi = 1.8378770664093453;
+constexpr double kStdEps = 1e-7;
+typedef double d4 __attribute__((ext_vector_type(4)));
+static_assert(CB % kThreads == 0, "W2 k-tile chunks must divide the block");
+
+template <int FP>
+constexpr size_t lds_bytes() {
+  return (2ull * BM * KP + 2ull * BN * KP + (size_t)BM * (FP + 2)) * sizeof(double);
+}
+
+template <int FP, bool VEC>
+__global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
+    const double* __restrict__ x, int64_t N, int F, const double* __restrict__ W1,
+    const double* __restrict__ b1, int H1, const double* __restrict__ W2,
+    const double* __restrict__ b2, int H2, const double* __restrict__ Wm,
+    const double* __restrict__ bm, const double* __restrict__ log_std,
+    const double* __restrict__ act, int A, double* __restrict__ h1_out,
+    double* __restrict__ z2_out, double* __restrict__ mu_out, double* __restrict__ logp_out) {
+  constexpr int XP = FP + 2;  // padded x row: lanes of a fragment read hit distinct banks
+  extern __shared__ double lds[];
+  double* sA = lds;                    // [2][BM][KP]  h1 k-tile (A operand)
+  double* sB = sA + 2 * BM * KP;       // [2][BN][KP]  W2 k-tile (B operand)
+  double* sX = sB + 2 * BN * KP;       // [BM][XP]     x rows
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave / WC, wc = wave % WC;
+  const int fr = lane & 15, g = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * BM;
+  const int nkt = (H1 + KT - 1) / KT;
+
+  // Operand loads below read a clamped (always valid) address and zero the value afterwards:
+  // no branch around a load, so the compiler does not serialise them behind vmcnt waits.
+  for (int e = tid; e < BM * FP; e += kThreads) {
+    const int r = e / FP, f = e % FP;
+    const int64_t rr = min<int64_t>(row0 + r, N - 1);
+    const double v = x[rr * F + min(f, F - 1)];
+    sX[r * XP + f] = (f < F && row0 + r < N) ? v : 0.0;
+  }
+
+  // ---- layer 1 on waves 0..3 (one per SIMD): rows 16 w .. 16 w + 15 of the block ----------
+  double w1n[FP / 4];
+  auto w1_load = [&](int kt) __attribute__((always_inline)) {
+    const int c = kt * KT + fr;
+    const double* wr1 = W1 + (int64_t)min(c, H1 - 1) * F;
+#pragma unroll
+    for (int s = 0; s < FP / 4; ++s) w1n[s] = wr1[min(4 * s + g, F - 1)];  // masked in h1_gen
+  };
+  auto h1_gen = [&](int kt, int buf) __attribute__((always_inline)) {
+    // two independent MFMA chains (even / odd k-steps) halve the dependent latency
+    // up to four independent MFMA chains (k-steps s mod 4) shorten the dependent latency.
+    // x columns >= F are zero in LDS, so a clamped (duplicate) W1 value there contributes 0;
+    // only the rows c >= H1 of a partial last tile need masking (below, after the bias)
+    constexpr int NS = FP / 4, NCH = NS < 4 ? NS : 4;
+    d4 hc[NCH];
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) hc[u] = d4{0.0, 0.0, 0.0, 0.0};
+    const double* xr = sX + (wave * 16 + fr) * XP + g;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      hc[s % NCH] = __builtin_amdgcn_mfma_f64_16x16x4f64(xr[4 * s], w1n[s], hc[s % NCH], 0, 0, 0);
+    d4 h = hc[0];
+#pragma unroll
+    for (int u = 1; u < NCH; ++u) h += hc[u];
+    const int c = kt * KT + fr;
+    const double bc = c < H1 ? b1[c] : 0.0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int r = wave * 16 + g + 4 * q;
+      const double v = c < H1 ? fmax(h[q] + bc, 0.0) : 0.0;
+      sA[(buf * BM + r) * KP + fr] = v;
+      if (c < H1 && row0 + r < N) h1_out[(row0 + r) * H1 + c] = v;
+    }
+  };
+
+  // ---- W2 k-tiles: global -> registers -> LDS ---------------------------------------------
+  double2 rb[PB];
+  auto b_load = [&](int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+      const int ch = tid + p * kThreads, r = ch >> 3, k = kt * KT + 2 * (ch & 7);
+      const double* row = W2 + (int64_t)min(r, H2 - 1) * H1;
+      double2 v;
+      if constexpr (VEC)  // H1 even: k < H1 implies k + 1 < H1, 16-B aligned pair
+        v = *reinterpret_cast<const double2*>(row + min(k, H1 - 2));
+      else
+        v = double2{row[min(k, H1 - 1)], row[min(k + 1, H1 - 1)]};
+      rb[p] = v;  // masked in b_store: a select here would wait for the load at once
+    }
+  };
+  auto b_store = [&](int kt, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < PB; ++p) {
+      const int ch = tid + p * kThreads, r = ch >> 3, k = kt * KT + 2 * (ch & 7);
+      double2 v = rb[p];
+      if (r >= H2 || k >= H1) v = double2{0.0, 0.0};
+      if (k + 1 >= H1) v.y = 0.0;
+      *reinterpret_cast<double2*>(sB + (buf * BN + r) * KP + 2 * (ch & 7)) = v;
+    }
+  };
+
+  d4 acc[FR][FC];
+#pragma unroll
+  for (int i = 0; i < FR; ++i)
+#pragma unroll
+    for (int j = 0; j < FC; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
+
+  b_load(0);
+  if (wave < 4) w1_load(0);
+  __syncthreads();  // sX
+  if (wave < 4) {
+    h1_gen(0, 0);
+    if (nkt > 1) w1_load(1);
+  }
+  b_store(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nkt) {
+      b_load(kt + 1);
+      // layer 1 of the NEXT k-tile ahead of this tile's GEMM, so its short dependent MFMA
+      // chains, bias/ReLU and HBM stores overlap the GEMM instead of stalling the barrier.
+      // sA[buf ^ 1] was last read in iteration kt - 1, behind that iteration's barrier.
+      if (wave < 4) {
+        h1_gen(kt + 1, buf ^ 1);
+        if (kt + 2 < nkt) w1_load(kt + 2);
+      }
+    }
+    double2 a[FR][2], b[FC][2];
+#pragma unroll
+    for (int i = 0; i < FR; ++i) {
+      const double* p = sA + (buf * BM + wr * FR * 16 + i * 16 + fr) * KP + 4 * g;
+      a[i][0] = *reinterpret_cast<const double2*>(p);
+      a[i][1] = *reinterpret_cast<const double2*>(p + 2);
+    }
+#pragma unroll
+    for (int j = 0; j < FC; ++j) {
+      const double* p = sB + (buf * BN + wc * FC * 16 + j * 16 + fr) * KP + 4 * g;
+      b[j][0] = *reinterpret_cast<const double2*>(p);
+      b[j][1] = *reinterpret_cast<const double2*>(p + 2);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int i = 0; i < FR; ++i) {
+        const double av = (s & 1) ? a[i][s >> 1].y : a[i][s >> 1].x;
+#pragma unroll
+        for (int j = 0; j < FC; ++j) {
+          const double bv = (s & 1) ? b[j][s >> 1].y : b[j][s >> 1].x;
+          acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    if (kt + 1 < nkt) b_store(kt + 1, buf ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: z2 out, then the head on relu(z2 + b2) -----------------------------------
+  // C/D map of the f64 16x16x4 MFMA: col = lane & 15, row = (lane >> 4) + 4 q.
+  double b2v[FC];
+#pragma unroll
+  for (int j = 0; j < FC; ++j) {
+    const int c = wc * FC * 16 + j * 16 + fr;
+    b2v[j] = c < H2 ? b2[c] : 0.0;
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t r = row0 + wr * FR * 16 + i * 16 + g + 4 * q;
+        if (c < H2 && r < N) z2_out[r * H2 + c] = acc[i][j][q];
+      }
+  }
+  double* sMu = sB;  // [WC][BM][kAChunk]; the loop's last barrier retired every sB read
+  const int er = tid >> 3, ea = tid & 7;  // combine step: row er of the block, action slot ea
+  double lp = 0.0;
+  for (int a0 = 0; a0 < A; a0 += kAChunk) {
+    double wmv[FC][kAChunk];
+#pragma unroll
+    for (int j = 0; j < FC; ++j) {
+      const int c = wc * FC * 16 + j * 16 + fr;
+#pragma unroll
+      for (int a = 0; a < kAChunk; ++a)
+        wmv[j][a] = (c < H2 && a0 + a < A) ? Wm[(int64_t)(a0 + a) * H2 + c] : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double p[kAChunk];
+#pragma unroll
+        for (int a = 0; a < kAChunk; ++a) p[a] = 0.0;
+#pragma unroll
+        for (int j = 0; j < FC; ++j) {
+          const double rv = fmax(acc[i][j][q] + b2v[j], 0.0);
+#pragma unroll
+          for (int a = 0; a < kAChunk; ++a) p[a] = fma(rv, wmv[j][a], p[a]);
+        }
+        // reduce-scatter over the 16 lanes of the row: halving exchanges on lane bits 8, 4, 2
+        // leave lane l with component ((l>>3)&1)*4 + ((l>>2)&1)*2 + ((l>>1)&1), then bit 1
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          const bool up = (fr & 8) != 0;
+          const double send = up ? p[a] : p[a + 4];
+          p[a] = (up ? p[a + 4] : p[a]) + __shfl_xor(send, 8, kWave);
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const bool up = (fr & 4) != 0;
+          const double send = up ? p[a] : p[a + 2];
+          p[a] = (up ? p[a + 2] : p[a]) + __shfl_xor(send, 4, kWave);
+        }
+        {
+          const bool up = (fr & 2) != 0;
+          const double send = up ? p[0] : p[1];
+          p[0] = (up ? p[1] : p[0]) + __shfl_xor(send, 2, kWave);
+        }
+        p[0] += __shfl_xor(p[0], 1, kWave);
+        const int comp = ((fr >> 3) & 1) * 4 + ((fr >> 2) & 1) * 2 + ((fr >> 1) & 1);
+        if ((fr & 1) == 0) {
+          const int rl = wr * FR * 16 + i * 16 + g + 4 * q;
+          sMu[(wc * BM + rl) * kAChunk + comp] = p[0];
+        }
+      }
+    __syncthreads();
+    {
+      const int a = a0 + ea;
+      const int64_t r = row0 + er;
+      double term = 0.0;
+      if (a < A && r < N) {
+        double m = sMu[(0 * BM + er) * kAChunk + ea];
+#pragma unroll
+        for (int w = 1; w < WC; ++w) m += sMu[(w * BM + er) * kAChunk + ea];
+        m += bm[a];
+        const double lsa = log_std[a];
+        const double sd = exp(lsa) + kStdEps;
+        const double d = act[r * A + a] - m;
+        mu_out[r * A + a] = m;
+        term = -0.5 * (kLog2Pi + 2.0 * lsa + d * d / (sd * sd));
+      }
+      term += __shfl_xor(term, 4, kWave);
+      term += __shfl_xor(term, 2, kWave);
+      term += __shfl_xor(term, 1, kWave);
+      lp += term;
+    }
+    __syncthreads();
+  }
+  if (ea == 0 && row0 + er < N) logp_out[row0 + er] = lp;
+}
+
+template <int FP, bool VEC>
+int launch(const double* x, int64_t n, int F, const double* W1, const double* b1, int H1,
+           const double* W2, const double* b2, int H2, const double* Wm, const double* bm,
+           const double* log_std, const double* act, int A, double* h1, double* z2, double* mu,
+           double* logp, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    MEPOL_HIP(hipFuncSetAttribute((const void*)policy_fwd_kernel<FP, VEC>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds_bytes<FP>()));
+    attr = true;
+  }
+  const unsigned blocks = (unsigned)((n + BM - 1) / BM);
+  hipLaunchKernelGGL((policy_fwd_kernel<FP, VEC>), dim3(blocks), dim3(kThreads), lds_bytes<FP>(), st,
+                     x, n, F, W1, b1, H1, W2, b2, H2, Wm, bm, log_std, act, A, h1, z2, mu, logp);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace pfwd
+}  // namespace mepol
+
+extern "C" int mepol_policy_forward(const double* x, int64_t n, int in_features,
+                                    const double* W1, const double* b1, int hidden0,
+                                    const double* W2, const double* b2, int hidden1,
+                                    const double* Wm, const double* bm, const double* log_std,
+                                    const double* actions, int action_dim, double* h1_out,
+                                    double* z2_out, double* mu_out, double* logp_out,
+                                    void* stream) {
+  using namespace mepol::pfwd;
+  if (n < 0 || in_features <= 0 || in_features > 64 || hidden0 <= 0 || hidden1 <= 0 ||
+      hidden1 > BN || action_dim <= 0 || !x || !W1 || !b1 || !W2 || !b2 || !Wm || !bm ||
+      !log_std || !actions || !h1_out || !z2_out || !mu_out || !logp_out ||
+      ((uintptr_t)W2 & 15)) {
+    mepol::set_error("mepol_policy_forward: bad arguments (in_features <= 64, hidden1 <= %d)",
+                     BN);
+    return mepol::kErrBadArg;
+  }
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+#define MEPOL_PF(FPV)                                                                        \
+  return (hidden0 % 2 == 0 && hidden0 >= 2)                                                  \
+             ? launch<FPV, true>(x, n, in_features, W1, b1, hidden0, W2, b2, hidden1, Wm, bm, \
+                                 log_std, actions, action_dim, h1_out, z2_out, mu_out,        \
+                                 logp_out, st)                                                \
+             : launch<FPV, false>(x, n, in_features, W1, b1, hidden0, W2, b2, hidden1, Wm,    \
+                                  bm, log_std, actions, action_dim, h1_out, z2_out, mu_out,   \
+                                  logp_out, st)
+  if (in_features <= 4) MEPOL_PF(4);
+  if (in_features <= 8) MEPOL_PF(8);
+  if (in_features <= 16) MEPOL_PF(16);
+  if (in_features <= 32) MEPOL_PF(32);
+  if (in_features <= 48) MEPOL_PF(48);
+  MEPOL_PF(64);
+#undef MEPOL_PF
+}

@@ -242,6 +242,47 @@ def head_backward(grad_logp, z, Wm, log_std, act, mu, bz=None, need_dz=True, ws=
     return dz, dWm, dbm, dls, dbz
 
 
+POLICY_FWD_MAX_IN = 64
+POLICY_FWD_MAX_H1 = 320
+
+
+def policy_forward_ok(in_features, hidden1):
+    return in_features <= POLICY_FWD_MAX_IN and hidden1 <= POLICY_FWD_MAX_H1
+
+
+def policy_forward(x, W1, b1, W2, b2, Wm, bm, log_std, act, h1_out=None, z2_out=None,
+                   mu_out=None, logp_out=None):
+    """One-kernel forward of the two-hidden-layer Gaussian policy: returns (h1, z2, mu, logp)
+    with h1 = relu(x W1^T + b1), z2 = h1 W2^T (pre-bias), mu = relu(z2 + b2) Wm^T + bm and
+    logp = sum_a log N(act | mu, exp(log_std) + 1e-7)."""
+    n, f = x.shape
+    h0, h1w, a = W1.shape[0], W2.shape[0], Wm.shape[0]
+    dev = x.device
+
+    def buf(t, shape):
+        return t if t is not None else torch.empty(shape, dtype=torch.float64, device=dev)
+
+    h1 = buf(h1_out, (n, h0))
+    z2 = buf(z2_out, (n, h1w))
+    mu = buf(mu_out, (n, a))
+    logp = buf(logp_out, (n,))
+    call("mepol_policy_forward", ptr(x), n, f, ptr(W1), ptr(b1), h0, ptr(W2), ptr(b2), h1w,
+         ptr(Wm), ptr(bm), ptr(log_std), ptr(act), a, ptr(h1), ptr(z2), ptr(mu), ptr(logp),
+         _stream())
+    return h1, z2, mu, logp
+
+
+def gemm_nt(A, B, bias=None, relu=False, out=None, variant=0):
+    """act(A B^T + bias) on the f64 matrix cores: A [n, k], B [m, k] (row-major, k even)."""
+    n, k = A.shape
+    m = B.shape[0]
+    assert B.shape[1] == k and A.stride(1) == 1 and B.stride(1) == 1
+    C = out if out is not None else torch.empty((n, m), dtype=torch.float64, device=A.device)
+    call("mepol_gemm_nt", ptr(A), n, k, A.stride(0), ptr(B), m, B.stride(0), ptr(bias),
+         int(relu), ptr(C), C.stride(0), variant, _stream())
+    return C
+
+
 def layer_forward(x, W, b, out=None):
     """h = relu(x W^T + b) for the policy's input layer (in_features <= 64)."""
     n, f = x.shape

@@ -80,6 +80,10 @@ class _HeadLogp(torch.autograd.Function):
 class _TwoLayerLogp(torch.autograd.Function):
     """log p(a | s) of the reference's 2-hidden-layer ReLU policy for a large batch:
 
+    fused    h1, z2 and the head in ONE kernel (csrc/policy_fwd.hip) when nf <= 64, h1 <= 320;
+             otherwise the three steps below
+    fused    layer 1, layer 2 and the head in ONE kernel (csrc/policy_fwd.hip) when nf <= 64
+             and h1 <= 320; otherwise the three steps:
     layer 1  h1 = relu(x W1^T + b1)            HIP (csrc/mlp.hip), bias + ReLU fused
     layer 2  z2 = h1 W2^T                       rocBLAS GEMM without bias
     head     logp(relu(z2 + b2) Wm^T + bm)      HIP (csrc/head.hip), b2 + ReLU folded in
@@ -90,9 +94,13 @@ class _TwoLayerLogp(torch.autograd.Function):
     def forward(ctx, x, W1, b1, W2, b2, Wm, bm, log_std, actions):
         from . import ops
 
-        h1 = ops.layer_forward(x, W1, b1)
-        z2 = torch.mm(h1, W2.t())
-        mu, logp = ops.head_forward(z2, Wm, bm, log_std, actions, bz=b2)
+        if ops.policy_forward_ok(x.shape[1], W2.shape[0]):  # one kernel (csrc/policy_fwd.hip)
+            h1, z2, mu, logp = ops.policy_forward(x, W1, b1, W2.contiguous(), b2, Wm, bm,
+                                                  log_std, actions)
+        else:
+            h1 = ops.layer_forward(x, W1, b1)
+            z2 = torch.mm(h1, W2.t())
+            mu, logp = ops.head_forward(z2, Wm, bm, log_std, actions, bz=b2)
         ctx.save_for_backward(x, h1, z2, W2, b2, Wm, log_std, actions, mu)
         return logp
 

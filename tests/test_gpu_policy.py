@@ -77,3 +77,33 @@ def test_predict_matches_forward(cuda):
     torch.manual_seed(0)
     b = pol.predict(s)
     assert b.shape == (2,) and not torch.equal(a, b)
+
+
+@pytest.mark.parametrize("n,nf,hidden,a", [(1000, 29, [400, 300], 8), (777, 2, [300, 300], 2),
+                                           (513, 47, [400, 300], 17), (300, 63, [400, 300], 20),
+                                           (100, 5, [37, 45], 3), (65, 1, [16, 320], 32),
+                                           (64, 33, [401, 17], 9), (1, 4, [8, 8], 1)])
+def test_policy_forward_kernel_matches_torch(cuda, n, nf, hidden, a):
+    """mepol_policy_forward (csrc/policy_fwd.hip: layer 1 + z2 GEMM + head in one kernel) ==
+    the nn.Linear / ReLU / Gaussian log-density math of src/policy.py:21-51 in torch f64."""
+    from mepol_amd import ops
+    from mepol_amd import policy as P
+
+    torch.manual_seed(3)
+    pol = P.GaussianPolicy(hidden, nf, a, -0.4).cuda()
+    s = torch.randn(n, nf, dtype=torch.float64, device="cuda")
+    act = 0.5 * torch.randn(n, a, dtype=torch.float64, device="cuda")
+    W1, b1 = pol.net[0].weight.detach(), pol.net[0].bias.detach()
+    W2, b2 = pol.net[2].weight.detach(), pol.net[2].bias.detach()
+    Wm, bm = pol.mean.weight.detach(), pol.mean.bias.detach()
+    ls = pol.log_std.detach()
+    h1, z2, mu, logp = ops.policy_forward(s, W1, b1, W2, b2, Wm, bm, ls, act)
+    h1_ref = torch.relu(s @ W1.t() + b1)
+    z2_ref = h1_ref @ W2.t()
+    mu_ref = torch.relu(z2_ref + b2) @ Wm.t() + bm
+    std = torch.exp(ls) + 1e-7
+    lp_ref = torch.sum(-0.5 * (P.LOG_2PI + 2 * ls + (act - mu_ref) ** 2 / std ** 2), dim=1)
+    torch.testing.assert_close(h1, h1_ref, rtol=1e-13, atol=1e-13)
+    torch.testing.assert_close(z2, z2_ref, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(mu, mu_ref, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(logp, lp_ref, rtol=1e-12, atol=1e-11)

@@ -43,6 +43,31 @@ __global__ __launch_bounds__(256) void fma_loop(double* out, int iters) {
   out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+template <int J>
+__device__ __forceinline__ void fmac_bc(double& acc, double b, double a) {
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(acc)
+               : "v"(b), "v"(a), "n"(J));
+}
+
+// v_fmac_f64 with a DPP row broadcast of src0 (the VALU GEMM's inner instruction).
+__global__ __launch_bounds__(256) void dpp_loop(double* out, int iters) {
+  double acc[16];
+  for (int j = 0; j < 16; ++j) acc[j] = 0.0;
+  double a = threadIdx.x * 1e-3, b = 1.0 - threadIdx.x * 1e-4;
+  for (int i = 0; i < iters; ++i) {
+    fmac_bc<0>(acc[0], b, a); fmac_bc<1>(acc[1], b, a); fmac_bc<2>(acc[2], b, a);
+    fmac_bc<3>(acc[3], b, a); fmac_bc<4>(acc[4], b, a); fmac_bc<5>(acc[5], b, a);
+    fmac_bc<6>(acc[6], b, a); fmac_bc<7>(acc[7], b, a); fmac_bc<8>(acc[8], b, a);
+    fmac_bc<9>(acc[9], b, a); fmac_bc<10>(acc[10], b, a); fmac_bc<11>(acc[11], b, a);
+    fmac_bc<12>(acc[12], b, a); fmac_bc<13>(acc[13], b, a); fmac_bc<14>(acc[14], b, a);
+    fmac_bc<15>(acc[15], b, a);
+  }
+  double s = 0;
+  for (int j = 0; j < 16; ++j) s += acc[j];
+  out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
 // Interleaved: 4 f64 MFMAs + 8*R independent v_fma_f64 per iteration (co-issue check).
 template <int R>
 __global__ __launch_bounds__(256) void mixed_loop(double* out, int iters) {
@@ -108,6 +133,12 @@ int main() {
     hipEventElapsedTime(&ms, e0, e1);
     fl = (double)blocks * 256 * iters * 8 * 2.0;
     printf("v_fma_f64: %.3f ms  %.1f TF/s\n", ms, fl / ms / 1e9);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL(dpp_loop, dim3(blocks), dim3(256), 0, 0, out, iters / 2);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    hipEventElapsedTime(&ms, e0, e1);
+    printf("v_fmac_f64_dpp row_newbcast: %.3f ms  %.1f TF/s\n", ms, fl / ms / 1e9);
   }
   for (int rep = 0; rep < 2; ++rep) {
     float ms;
