@@ -5,14 +5,15 @@ An iteration of the reference's loop (src/algorithms/mepol.py:429-439) is
 (KL at theta_t+1).  For the reference's two-hidden-layer ReLU policy that whole sequence is a
 fixed list of device launches:
 
-    iw_forward -> entropy_forward -> entropy_gamma -> entropy_reverse_scan      (dH/dlogp)
-    head_backward -> split-K dW2 -> dh1 GEMM -> layer_backward                 (dH/dtheta)
+    entropy_gamma -> entropy_reverse_scan                                      (dH/dlogp)
+    head_backward -> dh1 GEMM -> layer_backward ; split-K dW2 (forked stream)  (dH/dtheta)
     optim_step (Adam / RMSprop)                                                (theta_t+1)
-    layer_forward -> GEMM -> head_forward                                      (logp at t+1)
-    iw_forward -> entropy_forward                                              (KL at t+1)
+    policy_forward (layer 1 + GEMM + head, one kernel)                         (logp at t+1)
+    iw_forward -> entropy_forward                     (KL at t+1, and H, dH/dW for the next)
 
-The forward at theta_t+1 is written into static buffers that the next replay's backward reads,
-so one captured graph replays every iteration and the host only reads the two control scalars
+The forward at theta_t+1, its importance weights and dH/dW are written into static buffers
+that the next replay's backward reads (``_prime`` fills them before the first replay), so one
+captured graph replays every iteration and the host only reads the two control scalars
 (H, KL) per iteration.  The Adam/RMSprop state lives in the caller's torch optimizer
 (``optimizer.state[p]``: ``step``, ``exp_avg``, ``exp_avg_sq`` / ``square_avg``), updated in
 place; its per-step scalars (bias corrections, learning rate) are written to a device buffer
@@ -116,10 +117,14 @@ class DeviceIteration:
         self.logp = torch.empty(self.N, **f64)
         self.fused_fwd = (ops.policy_forward_ok(self.x.shape[1], W2.shape[0])
                           and os.environ.get("MEPOL_FUSED_FWD", "1") != "0")
+        self.dh1_first = os.environ.get("MEPOL_DH1_FIRST", "1") != "0"
         self.neg_one = torch.full((), -1.0, **f64)
         self.scal = torch.zeros(8, **f64)
         self.scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
         self.vals = torch.zeros(2, **f64)
+        self.w_cur = torch.zeros(self.N, **f64)   # importance weights of logp(theta_t)
+        self.g_cur = torch.zeros(self.N, **f64)   # dH/dW at theta_t
+        self.out_cur = torch.zeros(4, **f64)      # entropy_forward sums at theta_t
         # scratch owned by this graph (never the eager per-stream cache, whose buffers can be
         # replaced while a captured graph still holds their addresses)
         self.ws_head = ops.head_workspace(self.N, W2.shape[0], Wm.shape[0], dev)
@@ -240,7 +245,6 @@ class DeviceIteration:
         cur.wait_stream(self.s_gemm)
         cur.wait_stream(self.s_head)
 
-    refresh = forward
 
     def _backward(self, grad):
         """(dW1, db1, dW2, db2, dWm, dbm, dls) from dH/dlogp: the _TwoLayerLogp backward.
@@ -261,15 +265,31 @@ class DeviceIteration:
                                                         need_dz=True, ws=self.ws_head)
             e_h = torch.cuda.Event()
             e_h.record(cur)
-            # dW2 (split-K GEMM) on a forked stream, concurrent with dh1 -> layer-1 backward:
-            # the memory-bound layer kernel overlaps the MFMA-bound GEMM.
-            self.fork.wait_event(e_h)
-            with torch.cuda.stream(self.fork):
-                dW2 = _weight_grad(dz2, self.h1[sl])
-            self.s_gemm.wait_event(e_h)
-            with torch.cuda.stream(self.s_gemm):
-                dh1 = torch.mm(dz2, W2)
-                dW1, db1 = ops.layer_backward(dh1, self.h1[sl], self.x[sl], ws=self.ws_layer)
+            if self.dh1_first:
+                # dh1 alone (MFMA-bound, whole GPU), then dW2 (MFMA-bound) on the fork
+                # concurrent with the HBM-bound layer-1 backward, which therefore leaves the
+                # critical path (dh1 -> layer-1 backward was its tail).
+                self.s_gemm.wait_event(e_h)
+                with torch.cuda.stream(self.s_gemm):
+                    dh1 = torch.mm(dz2, W2)
+                    e_d = torch.cuda.Event()
+                    e_d.record(self.s_gemm)
+                    dW1, db1 = ops.layer_backward(dh1, self.h1[sl], self.x[sl],
+                                                  ws=self.ws_layer)
+                self.fork.wait_event(e_d)
+                with torch.cuda.stream(self.fork):
+                    dW2 = _weight_grad(dz2, self.h1[sl])
+            else:
+                # dW2 (split-K GEMM) on a forked stream, concurrent with dh1 -> layer-1
+                # backward.
+                self.fork.wait_event(e_h)
+                with torch.cuda.stream(self.fork):
+                    dW2 = _weight_grad(dz2, self.h1[sl])
+                self.s_gemm.wait_event(e_h)
+                with torch.cuda.stream(self.s_gemm):
+                    dh1 = torch.mm(dz2, W2)
+                    dW1, db1 = ops.layer_backward(dh1, self.h1[sl], self.x[sl],
+                                                  ws=self.ws_layer)
             keep += [dz2, dh1]
             parts.append((dW1, db1, dW2, db2, dWm, dbm, dls))
         cur.wait_stream(self.fork)
@@ -284,10 +304,9 @@ class DeviceIteration:
         W1, b1, W2, b2, Wm, bm, ls = self.named
         nt, T, N, k = self.nt, self.T, self.N, self.k
         lt = self.logp.view(nt, T)
-        # entropy at theta_t and dH/dlogp (compute_entropy + loss.backward, mepol.py:273-278)
-        _, _, w, _ = ops.iw_forward(lt, self.logp_b, self.offsets, N)
-        out_h, _, g = ops.entropy_forward(w, self.idx32T, self.D, k, self.ns, self.G, self.B,
-                                          self.eps)
+        # dH/dlogp at theta_t (loss.backward, mepol.py:273-278) from the importance weights and
+        # dH/dW that the previous replay (or _prime) left for logp(theta_t)
+        w, g = self.w_cur, self.g_cur
         gamma, partials, nparts = ops.entropy_gamma(g, w, self.csr_off, self.csr_rows)
         grad = ops.entropy_reverse_scan(gamma, w, partials, nparts, self.offsets, nt, T,
                                         self.neg_one)
@@ -297,11 +316,34 @@ class DeviceIteration:
         grad_of = {id(p): g for p, g in zip(self.named, (dW1, db1, dW2, db2, dWm, dbm, dls))}
         ops.optim_step(self.kind, self.params, [grad_of[id(p)] for p in self.params], self.m,
                        self.v, self.scal)
-        # compute_kl at theta_t+1 (mepol.py:435, :157-174)
+        # compute_kl at theta_t+1 (mepol.py:435, :157-174).  The pass with the entropy
+        # constants also yields the KL sum (its terms do not depend on them) and the next
+        # iteration's H(theta_t+1) and dH/dW, so each replay needs one weights pass, not two.
         self.forward()
         _, _, w2, _ = ops.iw_forward(lt, self.logp_b, self.offsets, N)
-        out_k, _, _ = ops.entropy_forward(w2, self.idx32T, self.D, k, 1.0, 1.0, 0.0, self.eps)
-        torch.cat((out_h[:1], out_k[1:2]), out=self.vals)
+        out2, _, g2 = ops.entropy_forward(w2, self.idx32T, self.D, k, self.ns, self.G, self.B,
+                                          self.eps)
+        torch.cat((self.out_cur[:1], out2[1:2]), out=self.vals)
+        self.w_cur.copy_(w2)
+        self.g_cur.copy_(g2)
+        self.out_cur.copy_(out2)
+
+    @torch.no_grad()
+    def _prime(self):
+        """w, dH/dW and H for logp(theta) of the current parameters (before the first replay
+        and after a rejected step restored theta)."""
+        lt = self.logp.view(self.nt, self.T)
+        _, _, w, _ = ops.iw_forward(lt, self.logp_b, self.offsets, self.N)
+        out, _, g = ops.entropy_forward(w, self.idx32T, self.D, self.k, self.ns, self.G, self.B,
+                                        self.eps)
+        self.w_cur.copy_(w)
+        self.g_cur.copy_(g)
+        self.out_cur.copy_(out)
+
+    def refresh(self):
+        """Recompute the iteration's inputs that depend on theta (logp, w, dH/dW)."""
+        self.forward()
+        self._prime()
 
     def _warmup(self):
         """One eager pass on a side stream (allocator pools, library handles, kernel code)."""

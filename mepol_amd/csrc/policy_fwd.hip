@@ -35,7 +35,7 @@ static_assert(CB % kThreads == 0, "W2 k-tile chunks must divide the block");
 
 template <int FP>
 constexpr size_t lds_bytes() {
-  return (2ull * BM * KP + 2ull * BN * KP + (size_t)BM * (FP + 2)) * sizeof(double);
+  return (2ull * BM * KP + 2ull * BN * KP + (size_t)(BM + 2 * KT) * (FP + 2)) * sizeof(double);
 }
 
 template <int FP, bool VEC>
@@ -51,6 +51,7 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
   double* sA = lds;                    // [2][BM][KP]  h1 k-tile (A operand)
   double* sB = sA + 2 * BM * KP;       // [2][BN][KP]  W2 k-tile (B operand)
   double* sX = sB + 2 * BN * KP;       // [BM][XP]     x rows
+  double* sW = sX + BM * XP;           // [2][KT][XP]  W1 rows of a k-tile (layer-1 B operand)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WC, wc = wave % WC;
   const int fr = lane & 15, g = lane >> 4;
@@ -67,26 +68,38 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
   }
 
   // ---- layer 1 on waves 0..3 (one per SIMD): rows 16 w .. 16 w + 15 of the block ----------
-  double w1n[FP / 4];
+  // W1 rows of k-tile kt (16 x F): staged through LDS one tile ahead of the W2 tiles, so the
+  // layer-1 waves issue no global loads of their own (a wait for one would also wait for the
+  // h1 stores issued before it: vmcnt counts stores too)
+  constexpr int PW = (KT * FP + kThreads - 1) / kThreads;
+  double rw[PW];
   auto w1_load = [&](int kt) __attribute__((always_inline)) {
-    const int c = kt * KT + fr;
-    const double* wr1 = W1 + (int64_t)min(c, H1 - 1) * F;
 #pragma unroll
-    for (int s = 0; s < FP / 4; ++s) w1n[s] = wr1[min(4 * s + g, F - 1)];  // masked in h1_gen
+    for (int p = 0; p < PW; ++p) {
+      const int e = tid + p * kThreads, r = e / FP, f = e % FP;
+      rw[p] = W1[(int64_t)min(kt * KT + r, H1 - 1) * F + min(f, F - 1)];
+    }
+  };
+  auto w1_store = [&](int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int p = 0; p < PW; ++p) {
+      const int e = tid + p * kThreads, r = e / FP, f = e % FP;
+      if (e < KT * FP) sW[((kt & 1) * KT + r) * XP + f] = (kt * KT + r < H1 && f < F) ? rw[p] : 0.0;
+    }
   };
   auto h1_gen = [&](int kt, int buf) __attribute__((always_inline)) {
-    // two independent MFMA chains (even / odd k-steps) halve the dependent latency
     // up to four independent MFMA chains (k-steps s mod 4) shorten the dependent latency.
-    // x columns >= F are zero in LDS, so a clamped (duplicate) W1 value there contributes 0;
-    // only the rows c >= H1 of a partial last tile need masking (below, after the bias)
+    // (W1 rows >= H1 and columns >= F are zero in LDS)
     constexpr int NS = FP / 4, NCH = NS < 4 ? NS : 4;
     d4 hc[NCH];
 #pragma unroll
     for (int u = 0; u < NCH; ++u) hc[u] = d4{0.0, 0.0, 0.0, 0.0};
     const double* xr = sX + (wave * 16 + fr) * XP + g;
+    const double* wr1 = sW + ((kt & 1) * KT + fr) * XP + g;
 #pragma unroll
     for (int s = 0; s < NS; ++s)
-      hc[s % NCH] = __builtin_amdgcn_mfma_f64_16x16x4f64(xr[4 * s], w1n[s], hc[s % NCH], 0, 0, 0);
+      hc[s % NCH] = __builtin_amdgcn_mfma_f64_16x16x4f64(xr[4 * s], wr1[4 * s], hc[s % NCH], 0,
+                                                         0, 0);
     d4 h = hc[0];
 #pragma unroll
     for (int u = 1; u < NCH; ++u) h += hc[u];
@@ -97,7 +110,9 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
       const int r = wave * 16 + g + 4 * q;
       const double v = c < H1 ? fmax(h[q] + bc, 0.0) : 0.0;
       sA[(buf * BM + r) * KP + fr] = v;
+#ifndef MEPOL_PF_NO_H1STORE
       if (c < H1 && row0 + r < N) h1_out[(row0 + r) * H1 + c] = v;
+#endif
     }
   };
 
@@ -134,25 +149,25 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
     for (int j = 0; j < FC; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
 
   b_load(0);
-  if (wave < 4) w1_load(0);
-  __syncthreads();  // sX
-  if (wave < 4) {
-    h1_gen(0, 0);
-    if (nkt > 1) w1_load(1);
+  w1_load(0);
+  w1_store(0);
+  if (nkt > 1) {
+    w1_load(1);
+    w1_store(1);
   }
+  __syncthreads();  // sX, sW
+  if (wave < 4) h1_gen(0, 0);
   b_store(0, 0);
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int buf = kt & 1;
     if (kt + 1 < nkt) {
       b_load(kt + 1);
+      if (kt + 2 < nkt) w1_load(kt + 2);
       // layer 1 of the NEXT k-tile ahead of this tile's GEMM, so its short dependent MFMA
       // chains, bias/ReLU and HBM stores overlap the GEMM instead of stalling the barrier.
       // sA[buf ^ 1] was last read in iteration kt - 1, behind that iteration's barrier.
-      if (wave < 4) {
-        h1_gen(kt + 1, buf ^ 1);
-        if (kt + 2 < nkt) w1_load(kt + 2);
-      }
+      if (wave < 4) h1_gen(kt + 1, buf ^ 1);
     }
     double2 a[FR][2], b[FC][2];
 #pragma unroll
@@ -179,7 +194,10 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
         }
       }
     }
-    if (kt + 1 < nkt) b_store(kt + 1, buf ^ 1);
+    if (kt + 1 < nkt) {
+      b_store(kt + 1, buf ^ 1);
+      if (kt + 2 < nkt) w1_store(kt + 2);  // sW[kt & 1]: last read by h1_gen(kt), a barrier ago
+    }
     __syncthreads();
   }
 
@@ -201,6 +219,9 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
   double* sMu = sB;  // [WC][BM][kAChunk]; the loop's last barrier retired every sB read
   const int er = tid >> 3, ea = tid & 7;  // combine step: row er of the block, action slot ea
   double lp = 0.0;
+#ifdef MEPOL_PF_NO_HEAD
+  A = 0;
+#endif
   for (int a0 = 0; a0 < A; a0 += kAChunk) {
     double wmv[FC][kAChunk];
 #pragma unroll

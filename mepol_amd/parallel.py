@@ -287,6 +287,11 @@ class ShardedIteration(DeviceIteration):
                 and ep.N == self.N_global and ep.world == self.world
                 and ep.dist is self.dist and ep.group is self.group)
 
+    # the sharded body computes its weights from logp each replay (collectives), so a refresh
+    # is the forward alone
+    def refresh(self):
+        self.forward()
+
     def attach(self, ep, logp_b):
         self.ep = ep
         self.load(_LocalView(ep), logp_b)
