@@ -139,6 +139,17 @@ int mepol_policy_forward(const double* x, int64_t n, int in_features, const doub
                          const double* actions, int action_dim, double* h1_out, double* z2_out,
                          double* mu_out, double* logp_out, void* stream);
 
+/* Backward of the first layer fused into the dh1 GEMM: dW1 [h0, in] and db1 [h0] (nullable) of
+ * h1 = relu(x W1^T + b1) from dz2 [n, k] and W2t = W2^T [h0, k] (dh1 = dz2 W2 stays on chip,
+ * masked by h1 > 0 from the forward's h1 [n, h0]).  k even, in_features <= 63, dz2 and W2t
+ * 16-byte aligned; workspace from mepol_dh1_layer1_workspace_size.  Replaces the dh1
+ * torch.mm + threshold_backward + dW1/db1 reductions of loss.backward() (mepol.py:278). */
+int mepol_dh1_layer1_workspace_size(int64_t n, int hidden0, int in_features, size_t* bytes);
+int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double* W2t, int hidden0,
+                              const double* h1, const double* x, int in_features, double* dW1,
+                              double* db1, void* workspace, size_t workspace_bytes,
+                              void* stream);
+
 /* Hidden layer on the f64 matrix cores: C = act(A B^T + bias), A [n, k] (row stride lda),
  * B [m, k] (ldb), bias [m] (nullable), C [n, m] (ldc); act = ReLU when relu != 0.  k, lda, ldb
  * even and A, B 16-byte aligned.  variant 0 = default tiling.  Replaces the torch.mm /

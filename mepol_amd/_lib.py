@@ -51,6 +51,9 @@ SIGNATURES = {
     "mepol_policy_forward": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
                              _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                              _c_vp],
+    "mepol_dh1_layer1_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
+    "mepol_dh1_layer1_backward": [_c_vp, _c_i64, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
+                                  _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_gemm_nt": [_c_vp, _c_i64, _c_int, _c_i64, _c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_vp,
                       _c_i64, _c_int, _c_vp],
     "mepol_gemm_dpp": [_c_vp, _c_i64, _c_int, _c_i64, _c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_vp,

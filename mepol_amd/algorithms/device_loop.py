@@ -117,7 +117,9 @@ class DeviceIteration:
         self.logp = torch.empty(self.N, **f64)
         self.fused_fwd = (ops.policy_forward_ok(self.x.shape[1], W2.shape[0])
                           and os.environ.get("MEPOL_FUSED_FWD", "1") != "0")
-        self.dh1_first = os.environ.get("MEPOL_DH1_FIRST", "1") != "0"
+        self.dh1_first = os.environ.get("MEPOL_DH1_FIRST", "0") != "0"
+        self.fused_dh1 = (ops.dh1_layer1_ok(self.x.shape[1], W2.shape[0]) and not self.dh1_first
+                          and os.environ.get("MEPOL_FUSED_DH1", "1") != "0")
         self.neg_one = torch.full((), -1.0, **f64)
         self.scal = torch.zeros(8, **f64)
         self.scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
@@ -129,6 +131,7 @@ class DeviceIteration:
         # replaced while a captured graph still holds their addresses)
         self.ws_head = ops.head_workspace(self.N, W2.shape[0], Wm.shape[0], dev)
         self.ws_layer = ops.layer_workspace(self.N, W1.shape[1], W1.shape[0], dev)
+        self.ws_dh1 = ops.dh1_layer1_workspace(self.N, W1.shape[0], W1.shape[1], dev)
         self.graph = None
         self.fork = torch.cuda.Stream(device=dev)
         self.s_gemm = torch.cuda.Stream(device=dev)
@@ -281,15 +284,22 @@ class DeviceIteration:
                     dW2 = _weight_grad(dz2, self.h1[sl])
             else:
                 # dW2 (split-K GEMM) on a forked stream, concurrent with dh1 -> layer-1
-                # backward.
+                # backward (measured: faster than dh1 first with dW2 overlapping the layer-1
+                # backward, and than splitting dW2 across both phases).
                 self.fork.wait_event(e_h)
                 with torch.cuda.stream(self.fork):
                     dW2 = _weight_grad(dz2, self.h1[sl])
                 self.s_gemm.wait_event(e_h)
                 with torch.cuda.stream(self.s_gemm):
-                    dh1 = torch.mm(dz2, W2)
-                    dW1, db1 = ops.layer_backward(dh1, self.h1[sl], self.x[sl],
-                                                  ws=self.ws_layer)
+                    if self.fused_dh1:  # dh1 stays on chip (csrc/gemm.hip)
+                        dh1 = None
+                        dW1, db1 = ops.dh1_layer1_backward(dz2, W2.t().contiguous(),
+                                                           self.h1[sl], self.x[sl],
+                                                           ws=self.ws_dh1)
+                    else:
+                        dh1 = torch.mm(dz2, W2)
+                        dW1, db1 = ops.layer_backward(dh1, self.h1[sl], self.x[sl],
+                                                      ws=self.ws_layer)
             keep += [dz2, dh1]
             parts.append((dW1, db1, dW2, db2, dWm, dbm, dls))
         cur.wait_stream(self.fork)

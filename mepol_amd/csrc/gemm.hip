@@ -36,58 +36,62 @@ struct Cfg {
   static constexpr size_t kLds = 2ull * (BM + BN) * KP * sizeof(double);
 };
 
+// The main loop shared by the kernels below: acc[i][j] += A[rows of fragment i] B[cols of
+// fragment j]^T over all of K for the workgroup tile (row0, col0).  Operand loads read clamped
+// (always valid) addresses; out-of-range values are zeroed when the registers are written to
+// LDS, after the MFMA block, so no select waits on a load right after issuing it.
 template <int WR, int WC, int FR, int FC>
-__global__ __launch_bounds__(WR * WC * 64) void gemm_nt_kernel(
-    const double* __restrict__ A, int64_t N, int K, int64_t lda, const double* __restrict__ B,
-    int M, int64_t ldb, const double* __restrict__ bias, int relu, double* __restrict__ C,
-    int64_t ldc) {
+__device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int64_t N, int K,
+                                              int64_t lda, const double* __restrict__ B, int M,
+                                              int64_t ldb, int64_t row0, int col0, double* lds,
+                                              d4 (&acc)[FR][FC]) {
   using P = Cfg<WR, WC, FR, FC>;
   constexpr int T = P::kThreads, BM = P::BM, BN = P::BN;
-  extern __shared__ double lds[];
   double* sA = lds;                  // [2][BM][KP]
   double* sB = lds + 2 * BM * KP;    // [2][BN][KP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WC, wc = wave % WC;
-  const int ncb = (M + BN - 1) / BN;
-  const int tile = xcd_tile(blockIdx.x, gridDim.x);
-  const int64_t row0 = (int64_t)(tile / ncb) * BM;
-  const int col0 = (tile % ncb) * BN;
   const int nkt = (K + KT - 1) / KT;
+  const int k2 = K - 2;  // last 16-B aligned pair start (K even)
 
   double2 ra[P::PA], rb[P::PB];
   auto gload = [&](int kt) __attribute__((always_inline)) {
     const int kb = kt * KT;
 #pragma unroll
     for (int p = 0; p < P::PA; ++p) {
-      const int ch = tid + p * T, r = ch >> 3, k = kb + 2 * (ch & 7);
-      const int64_t g = row0 + r;
-      ra[p] = (ch < P::CA && g < N && k < K) ? *reinterpret_cast<const double2*>(A + g * lda + k)
-                                             : double2{0.0, 0.0};
+      const int ch = min(tid + p * T, P::CA - 1), r = ch >> 3, k = kb + 2 * (ch & 7);
+      ra[p] = *reinterpret_cast<const double2*>(A + min<int64_t>(row0 + r, N - 1) * lda +
+                                                min(k, k2));
     }
 #pragma unroll
     for (int p = 0; p < P::PB; ++p) {
-      const int ch = tid + p * T, r = ch >> 3, k = kb + 2 * (ch & 7);
-      const int c = col0 + r;
-      rb[p] = (ch < P::CB && c < M && k < K) ? *reinterpret_cast<const double2*>(B + c * ldb + k)
-                                             : double2{0.0, 0.0};
+      const int ch = min(tid + p * T, P::CB - 1), r = ch >> 3, k = kb + 2 * (ch & 7);
+      rb[p] = *reinterpret_cast<const double2*>(B + (int64_t)min(col0 + r, M - 1) * ldb +
+                                                min(k, k2));
     }
   };
-  auto lstore = [&](int buf) __attribute__((always_inline)) {
+  auto lstore = [&](int kt, int buf) __attribute__((always_inline)) {
+    const int kb = kt * KT;
 #pragma unroll
     for (int p = 0; p < P::PA; ++p) {
-      const int ch = tid + p * T;
-      if (ch < P::CA)
-        *reinterpret_cast<double2*>(sA + (buf * BM + (ch >> 3)) * KP + 2 * (ch & 7)) = ra[p];
+      const int ch = tid + p * T, r = ch >> 3, k = kb + 2 * (ch & 7);
+      if (ch < P::CA) {
+        const bool ok = row0 + r < N && k < K;
+        *reinterpret_cast<double2*>(sA + (buf * BM + r) * KP + 2 * (ch & 7)) =
+            ok ? ra[p] : double2{0.0, 0.0};
+      }
     }
 #pragma unroll
     for (int p = 0; p < P::PB; ++p) {
-      const int ch = tid + p * T;
-      if (ch < P::CB)
-        *reinterpret_cast<double2*>(sB + (buf * BN + (ch >> 3)) * KP + 2 * (ch & 7)) = rb[p];
+      const int ch = tid + p * T, r = ch >> 3, k = kb + 2 * (ch & 7);
+      if (ch < P::CB) {
+        const bool ok = col0 + r < M && k < K;
+        *reinterpret_cast<double2*>(sB + (buf * BN + r) * KP + 2 * (ch & 7)) =
+            ok ? rb[p] : double2{0.0, 0.0};
+      }
     }
   };
 
-  d4 acc[FR][FC];
 #pragma unroll
   for (int i = 0; i < FR; ++i)
 #pragma unroll
@@ -95,7 +99,7 @@ __global__ __launch_bounds__(WR * WC * 64) void gemm_nt_kernel(
 
   const int fr = lane & 15, g = lane >> 4;
   gload(0);
-  lstore(0);
+  lstore(0, 0);
   __syncthreads();
   for (int kt = 0; kt < nkt; ++kt) {
     const int buf = kt & 1;
@@ -125,9 +129,28 @@ __global__ __launch_bounds__(WR * WC * 64) void gemm_nt_kernel(
         }
       }
     }
-    if (kt + 1 < nkt) lstore(buf ^ 1);
+    if (kt + 1 < nkt) lstore(kt + 1, buf ^ 1);
     __syncthreads();
   }
+}
+
+template <int WR, int WC, int FR, int FC>
+__global__ __launch_bounds__(WR * WC * 64) void gemm_nt_kernel(
+    const double* __restrict__ A, int64_t N, int K, int64_t lda, const double* __restrict__ B,
+    int M, int64_t ldb, const double* __restrict__ bias, int relu, double* __restrict__ C,
+    int64_t ldc) {
+  using P = Cfg<WR, WC, FR, FC>;
+  constexpr int BM = P::BM, BN = P::BN;
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wr = wave / WC, wc = wave % WC;
+  const int fr = lane & 15, g = lane >> 4;
+  const int ncb = (M + BN - 1) / BN;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int64_t row0 = (int64_t)(tile / ncb) * BM;
+  const int col0 = (tile % ncb) * BN;
+  d4 acc[FR][FC];
+  gemm_mainloop<WR, WC, FR, FC>(A, N, K, lda, B, M, ldb, row0, col0, lds, acc);
 
   // C/D map of the f64 16x16x4 MFMA: col = lane & 15, row = (lane >> 4) + 4 q.
 #pragma unroll
@@ -146,6 +169,115 @@ __global__ __launch_bounds__(WR * WC * 64) void gemm_nt_kernel(
           C[r * ldc + c] = v;
         }
       }
+  }
+}
+
+// ---- dh1 GEMM + first-layer backward (GaussianPolicy.net[0], src/policy.py:21-26) ------------
+// dh1 = dz2 W2 is never written: the epilogue masks it with relu'(h1) (h1 > 0, read from the
+// forward's h1) and reduces dz1^T [x | 1] over the tile's rows on the matrix cores, i.e. the
+// tile's contribution to dW1 (and db1 in column F).  The MFMA accumulator of dh1 already is
+// the A operand of that product (its k index = row); x comes from HBM as the B operand.
+// Row-block partials part[rb][c][F + 1] are summed in a fixed order by layer1_reduce_kernel.
+// Tiling: 8 waves x (32 rows x 80 cols), 256 x 80 tile: 5 column tiles for h0 = 400.
+namespace l1b {
+constexpr int WR = 8, WC = 1, FR = 2, FC = 5;
+using P = Cfg<WR, WC, FR, FC>;
+}  // namespace l1b
+
+template <int NH>  // NH = ceil((F + 1) / 16) column groups of [x | 1]
+__global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
+    const double* __restrict__ dz2, int64_t N, int K, const double* __restrict__ W2t, int M,
+    const double* __restrict__ h1, const double* __restrict__ x, int F,
+    double* __restrict__ part) {
+  using namespace l1b;
+  constexpr int BM = P::BM, BN = P::BN, T = P::kThreads;
+  extern __shared__ double lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int fr = lane & 15, g = lane >> 4;
+  const int ncb = (M + BN - 1) / BN;
+  const int tile = xcd_tile(blockIdx.x, gridDim.x);
+  const int rb = tile / ncb;
+  const int64_t row0 = (int64_t)rb * BM;
+  const int col0 = (tile % ncb) * BN;
+  d4 acc[FR][FC];
+  gemm_mainloop<WR, WC, FR, FC>(dz2, N, K, K, W2t, M, K, row0, col0, lds, acc);
+
+  // B operands [x | 1] for k-step (i, q): lane (fr, g) holds x[row(i, q, g)][16 h + fr]
+  double xb[FR][4][NH];
+#pragma unroll
+  for (int i = 0; i < FR; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t r = row0 + wave * FR * 16 + i * 16 + 4 * q + g;
+      const double* xr = x + min<int64_t>(r, N - 1) * F;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) {
+        const int f = 16 * h + fr;
+        const double v = xr[min(f, F - 1)];
+        xb[i][q][h] = r < N ? (f < F ? v : (f == F ? 1.0 : 0.0)) : 0.0;
+      }
+    }
+  double* red = lds;  // [WR][NH][4][64]: the main loop's last barrier retired its LDS reads
+  constexpr int NE = NH * 4 * 64;
+#pragma unroll
+  for (int j = 0; j < FC; ++j) {
+    const int c = col0 + j * 16 + fr;
+    d4 dacc[NH];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) dacc[h] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        // accumulator element (row g + 4 q of fragment i, col fr) is A[m = fr][k = g] of
+        // k-step (i, q): rows 16 i + 4 q + g
+        const int64_t r = row0 + wave * FR * 16 + i * 16 + g + 4 * q;
+        const double hv = h1[min<int64_t>(r, N - 1) * M + min(c, M - 1)];
+        const double dz = (hv > 0.0 && c < M) ? acc[i][j][q] : 0.0;
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+          dacc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(dz, xb[i][q][h], dacc[h], 0, 0, 0);
+      }
+    // dacc[h][r'] = sum over the wave's rows of dz1[.][col0 + 16 j + g + 4 r'] * [x|1][16 h + fr]
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[((wave * NH + h) * 4 + q) * 64 + lane] = dacc[h][q];
+    __syncthreads();
+    for (int e = threadIdx.x; e < NE; e += T) {
+      double s = red[e];
+#pragma unroll
+      for (int w = 1; w < WR; ++w) s += red[w * NE + e];
+      const int l = e & 63, q = (e >> 6) & 3, h = e >> 8;
+      const int cc = col0 + j * 16 + (l >> 4) + 4 * q, f = 16 * h + (l & 15);
+      if (cc < M && f <= F) part[((int64_t)rb * M + cc) * (F + 1) + f] = s;
+    }
+    __syncthreads();
+  }
+}
+
+// dW[c][f] = sum_b part[b][c][f], db[c] = sum_b part[b][c][F]: blocks own 64 elements and
+// split the row blocks over their 4 waves (fixed order: per-wave strided sums, then waves).
+__global__ __launch_bounds__(256) void layer1_reduce_kernel(const double* __restrict__ part,
+                                                            int nb, int M, int F,
+                                                            double* __restrict__ dW,
+                                                            double* __restrict__ db) {
+  __shared__ double sh[4][64];
+  const int64_t m = (int64_t)M * (F + 1);
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + l;
+  double s = 0.0;
+  if (e < m)
+    for (int b = w; b < nb; b += 4) s += part[(int64_t)b * m + e];
+  sh[w][l] = s;
+  __syncthreads();
+  if (w == 0 && e < m) {
+    const double t = sh[0][l] + sh[1][l] + sh[2][l] + sh[3][l];
+    const int c = (int)(e / (F + 1)), f = (int)(e % (F + 1));
+    if (f < F)
+      dW[(int64_t)c * F + f] = t;
+    else if (db)
+      db[c] = t;
   }
 }
 
@@ -355,4 +487,64 @@ extern "C" int mepol_gemm_dpp(const double* A, int64_t n, int k, int64_t lda, co
     case 9: return launch_dpp<2, 1, 5>(A, n, k, lda, B, m, ldb, bias, relu, C, ldc, st);
     default: return mepol::kErrBadArg;
   }
+}
+
+// dW1 [m, F], db1 [m] (nullable) of h1 = relu(x W1^T + b1) given dz2 [n, k] and W2t = W2^T
+// [m, k] (dh1 = dz2 W2 = dz2 W2t^T, not materialised), the forward's h1 [n, m] and x [n, F].
+extern "C" int mepol_dh1_layer1_workspace_size(int64_t n, int m, int in_features,
+                                               size_t* bytes) {
+  using namespace mepol::gemm::l1b;
+  if (!bytes) return mepol::kErrBadArg;
+  *bytes = (size_t)((n + P::BM - 1) / P::BM) * m * (in_features + 1) * sizeof(double);
+  return 0;
+}
+
+extern "C" int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double* W2t,
+                                         int m, const double* h1, const double* x,
+                                         int in_features, double* dW1, double* db1,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
+  using namespace mepol::gemm::l1b;
+  using mepol::gemm::dh1_layer1_bwd_kernel;
+  const int F = in_features;
+  if (n <= 0 || k <= 0 || (k & 1) || m <= 0 || F <= 0 || F > 63 || !dz2 || !W2t || !h1 || !x ||
+      !dW1 || !workspace || ((uintptr_t)dz2 & 15) || ((uintptr_t)W2t & 15)) {
+    mepol::set_error("mepol_dh1_layer1_backward: bad arguments (k even, in_features <= 63, "
+                     "16-B aligned dz2 / W2t)");
+    return mepol::kErrBadArg;
+  }
+  const int nrb = (int)((n + P::BM - 1) / P::BM);
+  const size_t need = (size_t)nrb * m * (F + 1) * sizeof(double);
+  if (workspace_bytes < need) {
+    mepol::set_error("mepol_dh1_layer1_backward: workspace %zu < %zu", workspace_bytes, need);
+    return mepol::kErrWorkspace;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const int ncb = (m + P::BN - 1) / P::BN;
+  const unsigned tiles = (unsigned)((int64_t)nrb * ncb);
+  double* part = (double*)workspace;
+  const int nh = (F + 1 + 15) / 16;
+#define MEPOL_L1B(NHV)                                                                         \
+  do {                                                                                         \
+    static bool attr = false;                                                                  \
+    if (!attr) {                                                                               \
+      MEPOL_HIP(hipFuncSetAttribute((const void*)dh1_layer1_bwd_kernel<NHV>,                   \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)P::kLds)); \
+      attr = true;                                                                             \
+    }                                                                                          \
+    hipLaunchKernelGGL(dh1_layer1_bwd_kernel<NHV>, dim3(tiles), dim3(P::kThreads), P::kLds, st, \
+                       dz2, n, k, W2t, m, h1, x, F, part);                                     \
+  } while (0)
+  switch (nh) {
+    case 1: MEPOL_L1B(1); break;
+    case 2: MEPOL_L1B(2); break;
+    case 3: MEPOL_L1B(3); break;
+    default: MEPOL_L1B(4); break;
+  }
+#undef MEPOL_L1B
+  MEPOL_CHECK_LAUNCH();
+  const int64_t elems = (int64_t)m * (F + 1);
+  hipLaunchKernelGGL(mepol::gemm::layer1_reduce_kernel, dim3((unsigned)((elems + 63) / 64)),
+                     dim3(256), 0, st, part, nrb, m, F, dW1, db1);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
 }

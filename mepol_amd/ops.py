@@ -62,6 +62,15 @@ def layer_workspace(n, f, out, device):
     return torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=device)
 
 
+def dh1_layer1_workspace(n, h0, f, device):
+    """A caller-owned scratch buffer for dh1_layer1_backward at these sizes."""
+    import ctypes
+
+    nbytes = ctypes.c_size_t()
+    call("mepol_dh1_layer1_workspace_size", n, h0, f, ctypes.byref(nbytes))
+    return torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=device)
+
+
 def knn_plan(n_cand, n_query, d, kp1, split=0):
     import ctypes
 
@@ -270,6 +279,33 @@ def policy_forward(x, W1, b1, W2, b2, Wm, bm, log_std, act, h1_out=None, z2_out=
          ptr(Wm), ptr(bm), ptr(log_std), ptr(act), a, ptr(h1), ptr(z2), ptr(mu), ptr(logp),
          _stream())
     return h1, z2, mu, logp
+
+
+DH1_L1_MAX_IN = 63
+
+
+def dh1_layer1_ok(in_features, hidden1):
+    return in_features <= DH1_L1_MAX_IN and hidden1 % 2 == 0
+
+
+def dh1_layer1_backward(dz2, W2t, h1, x, ws=None):
+    """(dW1, db1) of h1 = relu(x W1^T + b1) from dz2 = dL/dz2 [n, h1w] and W2t = W2^T
+    [h0, h1w]: dh1 = dz2 W2 is reduced on chip (csrc/gemm.hip), never written."""
+    n, k = dz2.shape
+    h0 = W2t.shape[0]
+    f = x.shape[1]
+    assert W2t.shape[1] == k and h1.shape == (n, h0) and dz2.is_contiguous() and W2t.is_contiguous()
+    if ws is None:
+        import ctypes
+
+        nbytes = ctypes.c_size_t()
+        call("mepol_dh1_layer1_workspace_size", n, h0, f, ctypes.byref(nbytes))
+        ws = _workspace(x.device, nbytes.value, tag="dh1l1")
+    dW = torch.empty((h0, f), dtype=torch.float64, device=x.device)
+    db = torch.empty(h0, dtype=torch.float64, device=x.device)
+    call("mepol_dh1_layer1_backward", ptr(dz2), n, k, ptr(W2t), h0, ptr(h1), ptr(x), f, ptr(dW),
+         ptr(db), ptr(ws), ws.numel(), _stream())
+    return dW, db
 
 
 def gemm_nt(A, B, bias=None, relu=False, out=None, variant=0):

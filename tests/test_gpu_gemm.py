@@ -46,3 +46,24 @@ def test_gemm_nt_rejects_odd_k(cuda):
     A = torch.randn(10, 3, dtype=torch.float64, device="cuda")
     with pytest.raises(_lib.MepolInputError):
         ops.gemm_nt(A, A)
+
+
+@pytest.mark.parametrize("n,nf,h0,h1w", [(200, 29, 400, 300), (1000, 2, 300, 300),
+                                         (513, 47, 400, 300), (300, 63, 400, 300),
+                                         (77, 5, 37, 46), (4097, 15, 96, 80), (1, 16, 16, 2)])
+def test_dh1_layer1_backward_matches_torch(cuda, n, nf, h0, h1w):
+    """Fused dh1 GEMM + layer-1 backward == torch: dh1 = dz2 W2, dz1 = dh1 * (h1 > 0),
+    dW1 = dz1^T x, db1 = sum dz1 (nn.Linear/ReLU backward of src/policy.py:21-26)."""
+    from mepol_amd import ops
+
+    torch.manual_seed(n + nf)
+    x = torch.randn(n, nf, dtype=torch.float64, device="cuda")
+    W1 = torch.randn(h0, nf, dtype=torch.float64, device="cuda") * 0.3
+    b1 = torch.randn(h0, dtype=torch.float64, device="cuda") * 0.1
+    W2 = torch.randn(h1w, h0, dtype=torch.float64, device="cuda") * 0.1
+    h1 = torch.relu(x @ W1.t() + b1)
+    dz2 = torch.randn(n, h1w, dtype=torch.float64, device="cuda")
+    dW1, db1 = ops.dh1_layer1_backward(dz2, W2.t().contiguous(), h1, x)
+    dz1 = (dz2 @ W2) * (h1 > 0)
+    torch.testing.assert_close(dW1, dz1.t() @ x, rtol=1e-11, atol=1e-11)
+    torch.testing.assert_close(db1, dz1.sum(0), rtol=1e-11, atol=1e-11)
