@@ -1098,7 +1098,8 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
       }
     // split-f16 instantiations that stay below the 256-VGPR cap (at the cap the fragment
     // buffers of the asm-load pipeline are no longer safe from register copies)
-    const bool fits = P->LIST16 <= 40 && P->KS16 <= 3;
+    // (<3, 40> and every KS16 = 4 list size needed for kp1 > 21 reach the cap: excluded)
+    const bool fits = P->KS16 <= 3 && P->LIST16 <= (P->KS16 == 3 ? 32 : 40);
     P->mode = (!want_f32 && fits) ? 1 : 0;
     // f32: d + 1 fma-chain roundings, x4 margin.  split-f16: 3 K products per output summed in
     // f32 (<= 3K roundings), operand splitting 3 * 2^-22 = 12 * 2^-24, |c|^2 in f32 (d), x2.
