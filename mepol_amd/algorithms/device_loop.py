@@ -124,6 +124,11 @@ class DeviceIteration:
         self.scal = torch.zeros(8, **f64)
         self.scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
         self.vals = torch.zeros(2, **f64)
+        # theta at the start of the latest replay = the last accepted parameters (a rejected
+        # step is undone by the caller before the next replay): off_policy_optimization copies
+        # it into last_valid only when it needs it, not after every accepted step
+        self.shadow = [torch.empty_like(p) for p in self.params]
+        self.tracks_shadow = type(self)._body is DeviceIteration._body
         self.w_cur = torch.zeros(self.N, **f64)   # importance weights of logp(theta_t)
         self.g_cur = torch.zeros(self.N, **f64)   # dH/dW at theta_t
         self.out_cur = torch.zeros(4, **f64)      # entropy_forward sums at theta_t
@@ -182,8 +187,7 @@ class DeviceIteration:
         """torch.optim's host-side step bookkeeping for one step; returns the device scalars."""
         g = self.opt.param_groups[0]
         steps = [self.opt.state[p]["step"] for p in self.params]
-        for s in steps:
-            s += 1
+        torch._foreach_add_(steps, 1.0)  # one dispatch instead of one per parameter
         lr = g["lr"]
         h = self.scal_host
         h[0] = 1.0
@@ -258,6 +262,9 @@ class DeviceIteration:
         order (fixed, so the result is reproducible)."""
         W1, b1, W2, b2, Wm, bm, ls = self.named
         cur = torch.cuda.current_stream()
+        # W2^T for the fused dh1 kernel, on this stream: on a forked one the small copy kernel
+        # would queue behind the dW2 GEMM's workgroups
+        W2t = W2.t().contiguous() if self.fused_dh1 else None
         self.fork.wait_stream(cur)
         self.s_gemm.wait_stream(cur)
         parts, keep = [], []
@@ -293,9 +300,8 @@ class DeviceIteration:
                 with torch.cuda.stream(self.s_gemm):
                     if self.fused_dh1:  # dh1 stays on chip (csrc/gemm.hip)
                         dh1 = None
-                        dW1, db1 = ops.dh1_layer1_backward(dz2, W2.t().contiguous(),
-                                                           self.h1[sl], self.x[sl],
-                                                           ws=self.ws_dh1)
+                        dW1, db1 = ops.dh1_layer1_backward(dz2, W2t, self.h1[sl],
+                                                           self.x[sl], ws=self.ws_dh1)
                     else:
                         dh1 = torch.mm(dz2, W2)
                         dW1, db1 = ops.layer_backward(dh1, self.h1[sl], self.x[sl],
@@ -314,6 +320,7 @@ class DeviceIteration:
         W1, b1, W2, b2, Wm, bm, ls = self.named
         nt, T, N, k = self.nt, self.T, self.N, self.k
         lt = self.logp.view(nt, T)
+        torch._foreach_copy_(self.shadow, self.params)
         # dH/dlogp at theta_t (loss.backward, mepol.py:273-278) from the importance weights and
         # dH/dW that the previous replay (or _prime) left for logp(theta_t)
         w, g = self.w_cur, self.g_cur

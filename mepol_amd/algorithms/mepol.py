@@ -731,6 +731,10 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
             loop = device_loop.get(target_policy, optimizer, batch, k, G, B, ns, eps)
             loop.load(batch, batch.behavioral_logp(behavioral_policy))
             loop.refresh()
+    # device loop: the parameters before each replay's step are kept on the device (the last
+    # accepted ones), so last_valid is only written when a step is rejected and at the end
+    shadow = loop.shadow if loop is not None and getattr(loop, "tracks_shadow", False) else None
+    last_accepted = False
     while not kl_threshold_reached:
         if loop is not None:
             # policy_update + compute_kl as one graph replay; two scalars come back
@@ -761,11 +765,16 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
             kl = _np(kl)
 
         if not numeric_error and not kl_numeric_error and kl <= kl_threshold:
-            _copy_policy(last_valid_target_policy, target_policy)
+            if shadow is None:
+                _copy_policy(last_valid_target_policy, target_policy)
+            last_accepted = True
             num_off_iters += 1
             if on_accept is not None:
                 on_accept(num_off_iters, entropy, kl, learning_rate)
         else:
+            last_accepted = False
+            if shadow is not None:
+                _copy_params(last_valid_target_policy, shadow)
             if use_backtracking:
                 if not backtrack_iter == max_backtrack_try:
                     _copy_policy(target_policy, last_valid_target_policy)
@@ -783,6 +792,8 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
         if num_off_iters == max_off_iters:
             kl_threshold_reached = True
 
+    if shadow is not None and last_accepted:
+        _copy_policy(last_valid_target_policy, target_policy)
     with torch.no_grad():
         entropy = fns.compute_entropy(last_valid_target_policy, last_valid_target_policy, states,
                                       actions, num_traj, real_traj_lengths, distances, indices, k,
@@ -791,6 +802,12 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
 
 
 _BUILTIN_STEP_FNS = (policy_update, compute_kl)
+
+
+def _copy_params(dst, tensors):
+    """dst's parameters <- tensors (same order and shapes), one fused device copy."""
+    with torch.no_grad():
+        torch._foreach_copy_(list(dst.parameters()), list(tensors))
 
 
 def _copy_policy(dst, src):

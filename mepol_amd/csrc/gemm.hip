@@ -256,29 +256,43 @@ __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
   }
 }
 
-// dW[c][f] = sum_b part[b][c][f], db[c] = sum_b part[b][c][F]: blocks own 64 elements and
-// split the row blocks over their 4 waves (fixed order: per-wave strided sums, then waves).
+// dW[c][f] = sum_b part[b][c][f], db[c] = sum_b part[b][c][F] in two fixed-order stages: stage 1
+// sums row-block group g (kGroups of them, strided rows) for 64 elements per block; stage 2 sums
+// the groups in order.  (One block column per 64 elements with all row blocks serial was
+// latency-bound at 79 us for 782 x 12000 partials.)
+constexpr int kGroups = 16;
+
 __global__ __launch_bounds__(256) void layer1_reduce_kernel(const double* __restrict__ part,
                                                             int nb, int M, int F,
-                                                            double* __restrict__ dW,
-                                                            double* __restrict__ db) {
+                                                            double* __restrict__ grp) {
   __shared__ double sh[4][64];
   const int64_t m = (int64_t)M * (F + 1);
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t e = (int64_t)blockIdx.x * 64 + l;
+  const int gi = blockIdx.y;
   double s = 0.0;
   if (e < m)
-    for (int b = w; b < nb; b += 4) s += part[(int64_t)b * m + e];
+    for (int b = gi + kGroups * w; b < nb; b += 4 * kGroups) s += part[(int64_t)b * m + e];
   sh[w][l] = s;
   __syncthreads();
-  if (w == 0 && e < m) {
-    const double t = sh[0][l] + sh[1][l] + sh[2][l] + sh[3][l];
-    const int c = (int)(e / (F + 1)), f = (int)(e % (F + 1));
-    if (f < F)
-      dW[(int64_t)c * F + f] = t;
-    else if (db)
-      db[c] = t;
-  }
+  if (w == 0 && e < m) grp[(int64_t)gi * m + e] = sh[0][l] + sh[1][l] + sh[2][l] + sh[3][l];
+}
+
+__global__ __launch_bounds__(256) void layer1_reduce2_kernel(const double* __restrict__ grp,
+                                                             int M, int F,
+                                                             double* __restrict__ dW,
+                                                             double* __restrict__ db) {
+  const int64_t m = (int64_t)M * (F + 1);
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= m) return;
+  double t = 0.0;
+#pragma unroll
+  for (int g = 0; g < kGroups; ++g) t += grp[(int64_t)g * m + e];
+  const int c = (int)(e / (F + 1)), f = (int)(e % (F + 1));
+  if (f < F)
+    dW[(int64_t)c * F + f] = t;
+  else if (db)
+    db[c] = t;
 }
 
 template <int WR, int WC, int FR, int FC>
@@ -495,7 +509,8 @@ extern "C" int mepol_dh1_layer1_workspace_size(int64_t n, int m, int in_features
                                                size_t* bytes) {
   using namespace mepol::gemm::l1b;
   if (!bytes) return mepol::kErrBadArg;
-  *bytes = (size_t)((n + P::BM - 1) / P::BM) * m * (in_features + 1) * sizeof(double);
+  *bytes = ((size_t)((n + P::BM - 1) / P::BM) + mepol::gemm::kGroups) * m * (in_features + 1) *
+           sizeof(double);
   return 0;
 }
 
@@ -513,7 +528,7 @@ extern "C" int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, co
     return mepol::kErrBadArg;
   }
   const int nrb = (int)((n + P::BM - 1) / P::BM);
-  const size_t need = (size_t)nrb * m * (F + 1) * sizeof(double);
+  const size_t need = ((size_t)nrb + mepol::gemm::kGroups) * m * (F + 1) * sizeof(double);
   if (workspace_bytes < need) {
     mepol::set_error("mepol_dh1_layer1_backward: workspace %zu < %zu", workspace_bytes, need);
     return mepol::kErrWorkspace;
@@ -543,8 +558,13 @@ extern "C" int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, co
 #undef MEPOL_L1B
   MEPOL_CHECK_LAUNCH();
   const int64_t elems = (int64_t)m * (F + 1);
-  hipLaunchKernelGGL(mepol::gemm::layer1_reduce_kernel, dim3((unsigned)((elems + 63) / 64)),
-                     dim3(256), 0, st, part, nrb, m, F, dW1, db1);
+  double* grp = part + (size_t)nrb * elems;
+  hipLaunchKernelGGL(mepol::gemm::layer1_reduce_kernel,
+                     dim3((unsigned)((elems + 63) / 64), mepol::gemm::kGroups), dim3(256), 0, st,
+                     part, nrb, m, F, grp);
+  MEPOL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(mepol::gemm::layer1_reduce2_kernel, dim3((unsigned)((elems + 255) / 256)),
+                     dim3(256), 0, st, grp, m, F, dW1, db1);
   MEPOL_CHECK_LAUNCH();
   return 0;
 }
