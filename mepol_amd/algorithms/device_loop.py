@@ -123,6 +123,7 @@ class DeviceIteration:
         self.neg_one = torch.full((), -1.0, **f64)
         self.scal = torch.zeros(8, **f64)
         self.scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
+        self.scal_np = self.scal_host.numpy()
         self.vals = torch.zeros(2, **f64)
         # theta at the start of the latest replay = the last accepted parameters (a rejected
         # step is undone by the caller before the next replay): off_policy_optimization copies
@@ -189,7 +190,7 @@ class DeviceIteration:
         steps = [self.opt.state[p]["step"] for p in self.params]
         torch._foreach_add_(steps, 1.0)  # one dispatch instead of one per parameter
         lr = g["lr"]
-        h = self.scal_host
+        h = self.scal_np  # numpy view of the pinned buffer: element writes without dispatch
         h[0] = 1.0
         if self.kind == _ADAM:
             beta1, beta2 = g["betas"]
@@ -336,13 +337,12 @@ class DeviceIteration:
         # compute_kl at theta_t+1 (mepol.py:435, :157-174).  The pass with the entropy
         # constants also yields the KL sum (its terms do not depend on them) and the next
         # iteration's H(theta_t+1) and dH/dW, so each replay needs one weights pass, not two.
+        # (w_cur and g_cur were last read by this replay's gamma / reverse scan, above)
         self.forward()
-        _, _, w2, _ = ops.iw_forward(lt, self.logp_b, self.offsets, N)
-        out2, _, g2 = ops.entropy_forward(w2, self.idx32T, self.D, k, self.ns, self.G, self.B,
-                                          self.eps)
+        ops.iw_forward(lt, self.logp_b, self.offsets, N, w_out=self.w_cur)
+        out2, _, _ = ops.entropy_forward(self.w_cur, self.idx32T, self.D, k, self.ns, self.G,
+                                         self.B, self.eps, g_out=self.g_cur)
         torch.cat((self.out_cur[:1], out2[1:2]), out=self.vals)
-        self.w_cur.copy_(w2)
-        self.g_cur.copy_(g2)
         self.out_cur.copy_(out2)
 
     @torch.no_grad()

@@ -132,7 +132,7 @@ def knn_exact(cand, kp1, query=None, want_int64=True):
     return D, I, I32T
 
 
-def iw_forward(logp_t, logp_b, offsets, n_particles, normalize=True):
+def iw_forward(logp_t, logp_b, offsets, n_particles, normalize=True, w_out=None):
     """u = exp(segmented cumsum(logp_t - logp_b)); w = u / sum(u).
 
     logp_t/logp_b: f64 [nt, T_stride]; offsets: int64 [nt+1] particle offsets.
@@ -145,7 +145,8 @@ def iw_forward(logp_t, logp_b, offsets, n_particles, normalize=True):
     lb = logp_b.contiguous()
     u = torch.empty(n_particles, dtype=torch.float64, device=dev)
     ts = torch.empty(nt, dtype=torch.float64, device=dev)
-    w = torch.empty(n_particles, dtype=torch.float64, device=dev) if normalize else None
+    w = (w_out if w_out is not None else torch.empty(n_particles, dtype=torch.float64,
+                                                     device=dev)) if normalize else None
     U = torch.empty((), dtype=torch.float64, device=dev) if normalize else None
     call("mepol_iw_forward", ptr(lt), ptr(lb), nt, Ts, ptr(offsets), n_particles, ptr(u), ptr(ts),
          ptr(w), ptr(U), _stream())
@@ -158,7 +159,7 @@ def iw_normalize(u, U):
     return w
 
 
-def entropy_forward(w, idxT, D, k, ns, G, B, eps, n_w=None):
+def entropy_forward(w, idxT, D, k, ns, G, B, eps, n_w=None, g_out=None):
     """Fused compute_entropy + compute_kl forward.
 
     Returns (out4 f64[4] = {H, KL_unclamped, sum_term, sum_klterm}, W [n], g [n]).
@@ -172,7 +173,7 @@ def entropy_forward(w, idxT, D, k, ns, G, B, eps, n_w=None):
     nparts = _lib.load().mepol_entropy_partials_size(n)
     partials = torch.empty(max(2 * nparts, 2), dtype=torch.float64, device=dev)
     W = torch.empty(n, dtype=torch.float64, device=dev)
-    g = torch.empty(n, dtype=torch.float64, device=dev)
+    g = g_out if g_out is not None else torch.empty(n, dtype=torch.float64, device=dev)
     out4 = torch.empty(4, dtype=torch.float64, device=dev)
     call("mepol_entropy_forward", ptr(w.contiguous()), ptr(idxT), ptr(D.contiguous()), n, n_w, k,
          kp1, float(ns), float(G), float(B), float(eps), ptr(W), ptr(g), ptr(partials), ptr(out4),
