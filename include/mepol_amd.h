@@ -95,7 +95,8 @@ int mepol_csr_workspace_size(int64_t nq, int k, int64_t ncand, size_t* bytes);
 int mepol_csr_build(const int32_t* idxT, int64_t nq, int k, int64_t col_offset, int64_t ncand,
                     int64_t row_offset, int32_t* csr_off, int32_t* csr_rows, void* workspace,
                     size_t workspace_bytes, void* stream);
-/* gamma_j = sum_{i in CSR(j)} g_i ; partials[b] = block sums of gamma_j w_j. */
+/* gamma_j = sum_{i in CSR(j)} g_i ; partials[b] = block sums of gamma_j w_j, one per 16
+ * particles: partials holds ceil(16 n_own / 256) doubles. */
 int mepol_entropy_gamma(const double* g, const double* w_own, const int32_t* csr_off,
                         const int32_t* csr_rows, int64_t n_own, double* gamma_out,
                         double* partials, void* stream);
@@ -110,7 +111,7 @@ int mepol_entropy_reverse_scan(const double* gamma, const double* w, const doubl
  * in.  z [n, hidden] is the last hidden layer's PRE-activation WITHOUT its bias bz (nullable);
  * Wm [a_dim, hidden], bm/log_std [a_dim]; act [n, a_dim].  Forward writes mu [n, a_dim] and
  * logp [n].  Backward (grad_logp [n]) writes dz [n, hidden] (nullable), dWm, dbm, dlog_std and
- * dbz [hidden] (nullable).  Limits: hidden <= 512, a_dim <= 8. */
+ * dbz [hidden] (nullable).  Limits: hidden <= 512, a_dim <= 32. */
 int mepol_head_forward(const double* z, int64_t n, int hidden, const double* bz, const double* Wm,
                        const double* bm, const double* log_std, const double* act, int a_dim,
                        double* mu_out, double* logp_out, void* stream);
