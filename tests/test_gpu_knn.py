@@ -149,3 +149,19 @@ def test_knn_rejects_non_finite(cuda, bad, where):
     D, I, _ = ops.knn(torch.as_tensor(X, device="cuda"), 31)
     Do, Io = O.knn_exact(X, 31)
     assert np.array_equal(D.cpu().numpy(), Do) and np.array_equal(I.cpu().numpy(), Io)
+
+
+@pytest.mark.parametrize("env", [{"MEPOL_KNN_SAMPLE": "8"}, {"MEPOL_KNN_SAMPLE": "8", "MEPOL_KNN_FILTER": "0"},
+                                 {"MEPOL_KNN_PRECISION": "f32"}, {"MEPOL_KNN_SAMPLE": "4", "MEPOL_KNN_CAP": "256"}])
+def test_knn_optional_paths_bitexact(cuda, monkeypatch, env):
+    """The tuning switches (sampled bound + survivor filter, sampled bound + lists, the f32 MFMA
+    selection, a small survivor cap that sends queries to the exhaustive path) change only the
+    candidate screening: the certified f64 output stays bit-identical to the default path."""
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((40000, 29)).astype(np.float32)
+    D0, I0, _, _ = _knn(X, 31)
+    for key, val in env.items():
+        monkeypatch.setenv(key, val)
+    D1, I1, _, _ = _knn(X, 31)
+    assert np.array_equal(D0, D1)
+    assert np.array_equal(I0, I1)
