@@ -106,6 +106,19 @@ int mepol_entropy_reverse_scan(const double* gamma, const double* w, const doubl
                                int64_t num_traj, int64_t T_stride, const double* grad_H,
                                double* grad_logp, void* stream);
 
+/* Whole rollout of collect_particles (mepol.py:70-111, one call for all T steps) for the
+ * reference's 2-hidden-layer ReLU policy on a 2-feature env: one workgroup per trajectory.
+ * env_id 0 = MountainCar (init64 [n,2] f64), 1 = GridWorld (init32 [n,2] f32, a_dim = 2).
+ * W1 [h0,2], b1 [h0], W2t = W2^T [h0,h1], b2 [h1], Wm [a_dim,h1], bm, log_std [a_dim];
+ * noise [T,n,a_dim] f64 (a = mean + noise * exp(log_std), policy.py:59).  Writes states_rec
+ * [n,T+1,2] f32, actions_rec [n,T,a_dim] f32, visited [n,T,2] f64 (nullable: the env state after
+ * each step, for the heatmap) and final_state [n,2] f64 (nullable).  h0, h1 <= 512, a_dim <= 8. */
+int mepol_rollout_mlp(int env_id, const double* W1, const double* b1, int h0, const double* W2t,
+                      const double* b2, int h1, const double* Wm, const double* bm,
+                      const double* log_std, int a_dim, const double* init64, const float* init32,
+                      const double* noise, int64_t n, int64_t T, float* states_rec,
+                      float* actions_rec, double* visited, double* final_state, void* stream);
+
 /* ---- policy MLP (GaussianPolicy, src/policy.py:16-51) for the large-batch passes -----------
  * Gaussian head: mean layer + log-probability with the last hidden layer's bias and ReLU folded
  * in.  z [n, hidden] is the last hidden layer's PRE-activation WITHOUT its bias bz (nullable);

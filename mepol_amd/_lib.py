@@ -62,6 +62,9 @@ SIGNATURES = {
     "mepol_step_gridworld": [_c_vp, _c_vp, _c_i64, _c_vp],
     "mepol_rollout_step": [_c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_i64,
                            _c_i64, _c_vp, _c_vp, _c_vp, _c_vp],
+    "mepol_rollout_mlp": [_c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
+                          _c_int, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp,
+                          _c_vp],
     "mepol_optim_step": [_c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
 }
 _RESTYPES = {"mepol_last_error_string": ctypes.c_char_p}

@@ -26,6 +26,7 @@ import weakref
 import numpy as np
 import scipy.special
 import torch
+import torch.nn as nn
 
 from .. import ops
 from ..envs.wrappers import unwrap
@@ -110,6 +111,21 @@ def _rollout_graph(policy, env_id, init, T, a_dim, nf):
     return g
 
 
+def _rollout_mlp_layers(policy, nf, a_dim):
+    """((W1, b1), (W2, b2)) when the policy is the reference's nf = 2 -> [h0, h1] -> a ReLU MLP in
+    f64 that the one-launch rollout kernel covers (h <= 512, a <= 8); else None."""
+    if os.environ.get("MEPOL_ROLLOUT_FUSED", "1") == "0" or nf != 2 or a_dim > 8:
+        return None
+    if getattr(policy, "activation", None) is not nn.ReLU:
+        return None
+    layers = [m for m in policy.net if isinstance(m, nn.Linear)]
+    if len(layers) != 2 or any(m.weight.dtype != torch.float64 for m in layers):
+        return None
+    if layers[0].in_features != 2 or max(m.out_features for m in layers) > 512:
+        return None
+    return tuple((m.weight.detach(), m.bias.detach()) for m in layers)
+
+
 def collect_particles_device(env, policy, num_traj, traj_len, state_filter, generator=None,
                              visited=None, shard=None):
     """Rollout of num_traj trajectories of traj_len steps, batched on the policy's device.
@@ -149,6 +165,17 @@ def collect_particles_device(env, policy, num_traj, traj_len, state_filter, gene
             init = base.reset_batch_torch(total, dev, generator)[lo:hi]
             noise_all = torch.randn((T, total, a_dim), dtype=torch.float64, device=dev,
                                     generator=generator)
+            lin = _rollout_mlp_layers(policy, nf, a_dim)
+            if lin is not None:  # all T steps in one launch (csrc/envs.hip rollout_mlp_kernel)
+                (W1, b1), (W2, b2) = lin
+                ops.rollout_mlp(env_id, W1, b1, W2, b2, policy.mean.weight.detach(),
+                                policy.mean.bias.detach(), policy.log_std.detach(), init,
+                                noise_all[:, lo:hi], states, actions, visited)
+                rtl = torch.full((num_traj, 1), T, dtype=torch.int32, device=dev)
+                next_states = states[:, 1:, :].reshape(-1, nf)
+                if state_filter is not None:
+                    next_states = next_states[:, list(state_filter)]
+                return states, actions, rtl, next_states.contiguous()
             graph = _rollout_graph(policy, env_id, init, T, a_dim, nf) if visited is None else None
             if graph is not None:
                 states, actions = graph.run(init, noise_all[:, lo:hi])

@@ -129,6 +129,155 @@ __global__ void rollout_step_kernel(double* __restrict__ env_f64, float* __restr
   }
 }
 
+
+// ---- whole rollout in one launch -----------------------------------------------------------
+// One workgroup per trajectory runs all T steps of collect_particles (mepol.py:81-90) for the
+// reference's 2-hidden-layer ReLU policy: x -> relu(W1 x + b1) -> relu(W2 h1 + b2) -> mean
+// (policy.py:21-28, 53-61) -> a = mean + noise * exp(log_std) -> env step, with the states /
+// actions recorded as f32.  Thread j owns hidden column j; its W1 row, biases and mean-layer
+// column stay in registers, the first KR rows of W2^T (k-major, [h0][h1]) too, and the rest of
+// W2^T streams from L2 each step (coalesced: one 8-byte word per thread per k).  Replaces the
+// per-step launch sequence (3 GEMMs + bias/ReLU + rollout_step, ~58 us per step even as a
+// replayed graph) with ~3 barriers per step.
+constexpr int kRollMaxH = 512;
+constexpr int kRollMaxA = 8;
+
+template <int ENV, int KR, int U>
+__global__ __launch_bounds__(kRollMaxH) void rollout_mlp_kernel(
+    const double* __restrict__ W1, const double* __restrict__ b1, int h0,
+    const double* __restrict__ W2t, const double* __restrict__ b2, int h1,
+    const double* __restrict__ Wm, const double* __restrict__ bm,
+    const double* __restrict__ log_std, int a_dim, const double* __restrict__ init64,
+    const float* __restrict__ init32, const double* __restrict__ noise, int64_t n, int64_t T,
+    float* __restrict__ states_rec, float* __restrict__ actions_rec,
+    double* __restrict__ visited, double* __restrict__ final_state, int KL) {
+  extern __shared__ double sW2[];  // [KL][blockDim.x]: W2^T rows KR .. KR + KL - 1
+  __shared__ double sx[2];
+  __shared__ double sh1[kRollMaxH];
+  __shared__ double spart[kRollMaxH / 64][kRollMaxA];
+  const int64_t i = blockIdx.x;
+  const int j = threadIdx.x, lane = j & 63, wave = j >> 6, nw = blockDim.x >> 6;
+  const bool c0 = j < h0, c1 = j < h1;
+  const double w1a = c0 ? W1[2 * j] : 0.0, w1b = c0 ? W1[2 * j + 1] : 0.0;
+  const double bb1 = c0 ? b1[j] : 0.0, bb2 = c1 ? b2[j] : 0.0;
+  double wm[kRollMaxA];
+#pragma unroll
+  for (int a = 0; a < kRollMaxA; ++a) wm[a] = (c1 && a < a_dim) ? Wm[a * h1 + j] : 0.0;
+  double w2r[KR > 0 ? KR : 1];
+#pragma unroll
+  for (int k = 0; k < KR; ++k) w2r[k] = (c1 && k < h0) ? W2t[(int64_t)k * h1 + j] : 0.0;
+  for (int k = 0; k < KL; ++k) sW2[k * blockDim.x + j] = c1 ? W2t[(int64_t)(KR + k) * h1 + j] : 0.0;
+  double p = 0.0, v = 0.0;  // MountainCar state (thread 0)
+  float gx = 0.f, gy = 0.f;  // GridWorld state (thread 0)
+  if (j == 0) {
+    if (ENV == 0) {
+      p = init64[2 * i];
+      v = init64[2 * i + 1];
+      sx[0] = p;
+      sx[1] = v;
+    } else {
+      gx = init32[2 * i];
+      gy = init32[2 * i + 1];
+      sx[0] = (double)gx;
+      sx[1] = (double)gy;
+    }
+    states_rec[(i * (T + 1)) * 2 + 0] = (float)sx[0];
+    states_rec[(i * (T + 1)) * 2 + 1] = (float)sx[1];
+  }
+  // thread 0: exp(log_std) once, and the next step's noise loaded a step ahead (its global
+  // latency would otherwise sit on the serial tail of every step)
+  double sd[kRollMaxA], nz[kRollMaxA];
+  if (j == 0) {
+    for (int a = 0; a < a_dim; ++a) {
+      sd[a] = exp(log_std[a]);
+      nz[a] = noise[i * a_dim + a];
+    }
+  }
+  __syncthreads();
+  for (int64_t t = 0; t < T; ++t) {
+    double nz_next[kRollMaxA];
+    if (j == 0 && t + 1 < T)
+      for (int a = 0; a < a_dim; ++a) nz_next[a] = noise[((t + 1) * n + i) * a_dim + a];
+    // layer 1 (nf = 2)
+    if (c0) sh1[j] = fmax(__dadd_rn(__dadd_rn(__dmul_rn(sx[0], w1a), __dmul_rn(sx[1], w1b)), bb1),
+                          0.0);
+    __syncthreads();
+    // layer 2: h2_j = relu(sum_k W2[j][k] h1[k] + b2[j]), k in order
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < KR; ++k) acc = fma(w2r[k], sh1[k], acc);
+    for (int k = 0; k < KL; ++k) acc = fma(sW2[k * blockDim.x + j], sh1[KR + k], acc);
+    {
+      // streamed rows: batches of U loads, the next batch in flight while this one is summed
+      // (L2 latency-bound: U rows per round trip)
+      const double* col = W2t + (c1 ? j : 0);
+      const int k0 = KR + KL;
+      int k = k0;
+      double cur[U], nxt[U];
+      const int kend = k0 + ((h0 - k0) / U) * U;
+      if (k < kend) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) cur[u] = col[(int64_t)(k + u) * h1];
+        for (; k < kend; k += U) {
+          if (k + U < kend) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) nxt[u] = col[(int64_t)(k + U + u) * h1];
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) acc = fma(c1 ? cur[u] : 0.0, sh1[k + u], acc);
+#pragma unroll
+          for (int u = 0; u < U; ++u) cur[u] = nxt[u];
+        }
+      }
+      for (; k < h0; ++k) acc = fma(c1 ? col[(int64_t)k * h1] : 0.0, sh1[k], acc);
+    }
+    const double h2 = c1 ? fmax(acc + bb2, 0.0) : 0.0;
+    // mean layer: per-wave partial sums over its 64 columns, then waves in order
+#pragma unroll
+    for (int a = 0; a < kRollMaxA; ++a) {
+      if (a < a_dim) {
+        double q = wm[a] * h2;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m, kWave);
+        if (lane == 0) spart[wave][a] = q;
+      }
+    }
+    __syncthreads();
+    if (j == 0) {
+      double act[kRollMaxA];
+      for (int a = 0; a < a_dim; ++a) {
+        double mu = spart[0][a];
+        for (int w = 1; w < nw; ++w) mu += spart[w][a];
+        mu += bm[a];
+        // output = mean + randn * exp(log_std)   (policy.py:59)
+        act[a] = __dadd_rn(mu, __dmul_rn(nz[a], sd[a]));
+        actions_rec[(i * T + t) * a_dim + a] = (float)act[a];
+      }
+      if (t + 1 < T)
+        for (int a = 0; a < a_dim; ++a) nz[a] = nz_next[a];
+      if (ENV == 0) {
+        MountainCar::step(p, v, act[0]);
+        sx[0] = p;
+        sx[1] = v;
+      } else {
+        GridWorld::step(gx, gy, act[0], act[1]);
+        sx[0] = (double)gx;
+        sx[1] = (double)gy;
+      }
+      states_rec[(i * (T + 1) + t + 1) * 2 + 0] = (float)sx[0];
+      states_rec[(i * (T + 1) + t + 1) * 2 + 1] = (float)sx[1];
+      if (visited) {
+        visited[(i * T + t) * 2 + 0] = sx[0];
+        visited[(i * T + t) * 2 + 1] = sx[1];
+      }
+    }
+    __syncthreads();
+  }
+  if (j == 0 && final_state) {
+    final_state[2 * i] = sx[0];
+    final_state[2 * i + 1] = sx[1];
+  }
+}
 }  // namespace envs
 }  // namespace mepol
 
@@ -172,6 +321,65 @@ extern "C" int mepol_rollout_step(int env_id, double* env_f64, float* env_f32, c
   else
     hipLaunchKernelGGL(rollout_step_kernel<1>, g, dim3(256), 0, st, env_f64, env_f32, mean, noise,
                        log_std, n, a_dim, t, T, states_rec, actions_rec, policy_in);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}
+
+// env_id 0 = MountainCar (init64 [n,2] f64), 1 = GridWorld (init32 [n,2] f32).  The policy is
+// nf = 2 -> [h0, h1] -> a_dim with ReLU: W1 [h0,2], b1, W2t = W2^T [h0,h1], b2, Wm [a,h1], bm,
+// log_std [a]; noise [T,n,a_dim] f64.  Writes states_rec [n,T+1,2] f32, actions_rec [n,T,a] f32,
+// visited [n,T,2] f64 (nullable), final_state [n,2] f64 (nullable).
+extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1, int h0,
+                                 const double* W2t, const double* b2, int h1, const double* Wm,
+                                 const double* bm, const double* log_std, int a_dim,
+                                 const double* init64, const float* init32, const double* noise,
+                                 int64_t n, int64_t T, float* states_rec, float* actions_rec,
+                                 double* visited, double* final_state, void* stream) {
+  if (n <= 0 || T <= 0) return 0;
+  if (h0 <= 0 || h1 <= 0 || h0 > kRollMaxH || h1 > kRollMaxH || a_dim <= 0 ||
+      a_dim > kRollMaxA || env_id < 0 || env_id > 1 || (env_id == 0 && !init64) ||
+      (env_id == 1 && (!init32 || a_dim != 2)) || !W1 || !b1 || !W2t || !b2 || !Wm || !bm ||
+      !log_std || !noise || !states_rec || !actions_rec) {
+    set_error("mepol_rollout_mlp: bad arguments (hidden <= %d, a_dim <= %d)", kRollMaxH,
+              kRollMaxA);
+    return kErrBadArg;
+  }
+  const int threads = ((h0 > h1 ? h0 : h1) + 63) / 64 * 64;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 g((unsigned)n);
+  const char* kr = getenv("MEPOL_ROLLOUT_KR");
+  const int want = kr ? atoi(kr) : 0;
+  const int kr_used = want >= 32 ? 32 : 0;
+  // W2^T rows kept in LDS after the register rows: up to ~150 KB (MEPOL_ROLLOUT_KL caps it)
+  const char* klv = getenv("MEPOL_ROLLOUT_KL");
+  int KL = (int)((150 * 1024) / ((size_t)threads * sizeof(double)));
+  if (klv) KL = std::min(KL, atoi(klv));
+  KL = std::max(0, std::min(KL, h0 - kr_used));
+  const size_t lds = (size_t)KL * threads * sizeof(double);
+  const char* uv = getenv("MEPOL_ROLLOUT_U");
+  const int u = uv ? atoi(uv) : 8;
+#define MEPOL_ROLL(E, KR, U)                                                                      \
+  do {                                                                                            \
+    static bool attr = false;                                                                     \
+    if (!attr) {                                                                                  \
+      MEPOL_HIP(hipFuncSetAttribute((const void*)rollout_mlp_kernel<E, KR, U>,                    \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));     \
+      attr = true;                                                                                \
+    }                                                                                             \
+    hipLaunchKernelGGL((rollout_mlp_kernel<E, KR, U>), g, dim3(threads), lds, st, W1, b1, h0, W2t, \
+                       b2, h1, Wm, bm, log_std, a_dim, init64, init32, noise, n, T, states_rec,   \
+                       actions_rec, visited, final_state, KL);                                    \
+  } while (0)
+  if (env_id == 0) {
+    if (kr_used >= 32) MEPOL_ROLL(0, 32, 8);
+    else if (u >= 16) MEPOL_ROLL(0, 0, 16);
+    else MEPOL_ROLL(0, 0, 8);
+  } else {
+    if (kr_used >= 32) MEPOL_ROLL(1, 32, 8);
+    else if (u >= 16) MEPOL_ROLL(1, 0, 16);
+    else MEPOL_ROLL(1, 0, 8);
+  }
+#undef MEPOL_ROLL
   MEPOL_CHECK_LAUNCH();
   return 0;
 }

@@ -387,5 +387,20 @@ def rollout_step(env_id, env_f64, env_f32, mean, noise, log_std, t, T, states_re
          _stream())
 
 
+def rollout_mlp(env_id, W1, b1, W2, b2, Wm, bm, log_std, init, noise, states_rec, actions_rec,
+                visited=None):
+    """All T steps of a batched MountainCar (env_id 0, init f64 [n,2]) / GridWorld (1, init f32)
+    rollout with the 2-hidden-layer ReLU policy in one launch; noise [T, n, a] f64."""
+    T, n, a_dim = noise.shape
+    h0, h1 = W1.shape[0], W2.shape[0]
+    W2t = W2.t().contiguous()
+    init64 = init.contiguous() if env_id == 0 else None
+    init32 = init.contiguous() if env_id == 1 else None
+    call("mepol_rollout_mlp", env_id, ptr(W1.contiguous()), ptr(b1), h0, ptr(W2t), ptr(b2), h1,
+         ptr(Wm.contiguous()), ptr(bm), ptr(log_std.contiguous()), a_dim, ptr(init64), ptr(init32),
+         ptr(noise.contiguous()), n, T, ptr(states_rec), ptr(actions_rec), ptr(visited), None,
+         _stream())
+
+
 def volume_constant(ns, G):
     return math.pi ** (ns / 2) / G

@@ -99,11 +99,14 @@ def test_collect_particles_contract(cuda):
     assert np.array_equal(D.cpu().numpy(), Do) and np.array_equal(I.cpu().numpy(), Io)
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
 @pytest.mark.parametrize("env_name", ["mountaincar", "gridworld"])
-def test_rollout_graph_and_shards_match_eager(cuda, monkeypatch, env_name):
+def test_rollout_graph_and_shards_match_eager(cuda, monkeypatch, env_name, fused):
     """The graph-replayed rollout == the eager per-step loop (bitwise), and the shards of a
     2- and 4-way trajectory split concatenate to the one-rank rollout (noise and initial states
-    are drawn for all trajectories up front)."""
+    are drawn for all trajectories up front).  fused = 1: the one-launch rollout kernel serves
+    both settings (no graph is captured)."""
+    monkeypatch.setenv("MEPOL_ROLLOUT_FUSED", fused)
     from mepol_amd.algorithms import mepol as M
     from mepol_amd.envs import ErgodicEnv, GridWorldContinuous, MountainCarContinuous
     from mepol_amd.policy import GaussianPolicy
@@ -124,7 +127,7 @@ def test_rollout_graph_and_shards_match_eager(cuda, monkeypatch, env_name):
         graph = roll(True)
         for x, y in zip(eager, graph):
             assert torch.equal(x, y)
-    assert len(M._ROLLOUT_GRAPHS.get(pol, {})) == 1
+    assert len(M._ROLLOUT_GRAPHS.get(pol, {})) == (1 if fused == "0" else 0)
     for world in (2, 4):
         parts = [roll(True, shard=(r, world)) for r in range(world)]
         assert torch.equal(torch.cat([p[0] for p in parts]), eager[0])
@@ -136,3 +139,43 @@ def test_rollout_graph_and_shards_match_eager(cuda, monkeypatch, env_name):
     eager2 = roll(False)
     graph2 = roll(True)
     assert torch.equal(eager2[0], graph2[0]) and not torch.equal(eager2[0], eager[0])
+
+
+@pytest.mark.parametrize("env", ["mountaincar", "gridworld"])
+@pytest.mark.parametrize("kr", ["0", "32", "64"])
+def test_rollout_mlp_kernel_matches_oracle(cuda, monkeypatch, env, kr):
+    """The one-launch rollout (mepol_rollout_mlp: policy MLP + noise + env step for all T steps,
+    one workgroup per trajectory) == the oracle's per-step rollout with the same injected noise,
+    to the rounding of the MLP's summation order; the register-cached W2 rows (MEPOL_ROLLOUT_KR)
+    do not change the result."""
+    from mepol_amd import ops
+    from mepol_amd.policy import GaussianPolicy
+
+    monkeypatch.setenv("MEPOL_ROLLOUT_KR", kr)
+    torch.manual_seed(5)
+    a_dim = 1 if env == "mountaincar" else 2
+    pol = GaussianPolicy([300, 300], 2, a_dim, -0.5 if env == "mountaincar" else -1.5).cuda()
+    nt, T = 16, 200
+    rng = np.random.default_rng(0)
+    if env == "mountaincar":
+        init = np.stack([rng.uniform(-0.6, -0.4, nt), np.zeros(nt)], 1)
+    else:
+        init = rng.uniform(-6, -4, (nt, 2)).astype(np.float32)
+    noise = rng.standard_normal((T, nt, a_dim))
+    sd = {k: v.detach().cpu().numpy() for k, v in pol.state_dict().items()}
+    S_ref, A_ref = O.rollout(env, sd, sd["log_std"], init, noise, T)
+    dev = "cuda"
+    states = torch.zeros((nt, T + 1, 2), dtype=torch.float32, device=dev)
+    actions = torch.zeros((nt, T, a_dim), dtype=torch.float32, device=dev)
+    visited = torch.zeros((nt, T, 2), dtype=torch.float64, device=dev)
+    l1, l2 = pol.net[0], pol.net[2]
+    ops.rollout_mlp(0 if env == "mountaincar" else 1, l1.weight.detach(), l1.bias.detach(),
+                    l2.weight.detach(), l2.bias.detach(), pol.mean.weight.detach(),
+                    pol.mean.bias.detach(), pol.log_std.detach(), torch.as_tensor(init, device=dev),
+                    torch.as_tensor(noise, dtype=torch.float64, device=dev), states, actions,
+                    visited)
+    S, A = states.cpu().numpy(), actions.cpu().numpy()
+    assert np.abs(A - A_ref).max() < 1e-5
+    assert (S == S_ref).mean() > 0.99
+    assert np.abs(S - S_ref).max() < 1e-3
+    assert np.array_equal(visited.cpu().numpy().astype(np.float32), S[:, 1:])
