@@ -173,6 +173,7 @@ __global__ __launch_bounds__(256) void entropy_finalize_kernel(const double* __r
 // per lane group (one lane per particle with a serial loop over ~k ids was latency-bound at
 // 85 us for C3).  Fixed order: lane sums over a stride of 16, then an xor tree.
 constexpr int kGammaLanes = 16;
+constexpr int64_t kGammaMaxBlocks = 1024;
 __global__ __launch_bounds__(256) void gamma_kernel(const double* __restrict__ g,
                                                     const double* __restrict__ w,
                                                     const int32_t* __restrict__ off,
@@ -180,19 +181,21 @@ __global__ __launch_bounds__(256) void gamma_kernel(const double* __restrict__ g
                                                     double* __restrict__ gamma,
                                                     double* __restrict__ partials) {
   __shared__ double sh[4];
-  const int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kGammaLanes;
   const int sub = threadIdx.x & (kGammaLanes - 1);
-  double gj = 0.0;
-  if (j < n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x / kGammaLanes;
+  double s = 0.0;
+  // grid-stride over particles (at most kGammaMaxBlocks partials for the reverse scan to read)
+  for (int64_t j = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / kGammaLanes; j < n;
+       j += stride) {
+    double gj = 0.0;
     const int32_t b = off[j], e = off[j + 1];
     for (int32_t x = b + sub; x < e; x += kGammaLanes) gj += g[rows[x]];
-  }
 #pragma unroll
-  for (int m = kGammaLanes / 2; m >= 1; m >>= 1) gj += __shfl_xor(gj, m, kWave);
-  double s = 0.0;
-  if (j < n && sub == 0) {
-    gamma[j] = gj;
-    s = gj * w[j];
+    for (int m = kGammaLanes / 2; m >= 1; m >>= 1) gj += __shfl_xor(gj, m, kWave);
+    if (sub == 0) {
+      gamma[j] = gj;
+      s += gj * w[j];
+    }
   }
   s = wave_sum(s);
   const int wv = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -309,7 +312,7 @@ extern "C" int mepol_entropy_forward(const double* w, const int32_t* idxT, const
 extern "C" int mepol_entropy_gamma(const double* g, const double* w_own, const int32_t* csr_off,
                                    const int32_t* csr_rows, int64_t n_own, double* gamma_out,
                                    double* partials, void* stream) {
-  const int64_t nb = (n_own * kGammaLanes + 255) / 256;
+  const int64_t nb = std::min<int64_t>((n_own * kGammaLanes + 255) / 256, kGammaMaxBlocks);
   if (nb == 0) return 0;
   hipLaunchKernelGGL(gamma_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, g, w_own,
                      csr_off, csr_rows, n_own, gamma_out, partials);
