@@ -44,6 +44,10 @@ WORKLOADS = {
                name="C4 Humanoid-shaped MEPOL epoch (k-NN + off-policy loop + final H)"),
     "C5": dict(COMMON, num_traj=10000, traj_len=50, nf=63, a=20, hidden=[400, 300], k=50, d=63,
                name="C5 HandReach-shaped MEPOL epoch (k-NN + off-policy loop + final H)"),
+    # one rank's particle share of C3 on 8 GPUs, run alone (no collectives, k-NN over its own
+    # 25k particles only): the compute floor of a rank in the 8-GPU strong-scaling run
+    "C3R8": dict(COMMON, num_traj=50, traj_len=500, nf=29, a=8, hidden=[400, 300], k=30, d=29,
+                 name="C3 per-rank share at 8 GPUs (25k particles, single GPU, no collectives)"),
     "C2": dict(COMMON, num_traj=20, traj_len=1000, nf=2, a=2, hidden=[300, 300], k=4, d=2,
                log_std_init=-1.5, env="GridWorld",
                name="C2 GridWorld MEPOL epoch (GPU rollout + k-NN + off-policy loop + final H)"),

@@ -34,6 +34,8 @@ extern "C" {
 
 const char* mepol_last_error_string(void);
 int mepol_abi_version(void);
+/* Stream-ordered copy (device <-> pinned host / device); captured as a graph memcpy node. */
+int mepol_memcpy_async(void* dst, const void* src, size_t bytes, void* stream);
 
 /* ---- k-NN ---------------------------------------------------------------------------------
  * Replaces src/algorithms/mepol.py:190-192

@@ -65,6 +65,7 @@ SIGNATURES = {
     "mepol_rollout_mlp": [_c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
                           _c_int, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp,
                           _c_vp],
+    "mepol_memcpy_async": [_c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_optim_step": [_c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
 }
 _RESTYPES = {"mepol_last_error_string": ctypes.c_char_p}

@@ -124,6 +124,8 @@ class DeviceIteration:
         self.scal = torch.zeros(8, **f64)
         self.scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
         self.scal_np = self.scal_host.numpy()
+        self.vals_host = torch.zeros(2, dtype=torch.float64).pin_memory()
+        self.vals_np = self.vals_host.numpy()
         self.vals = torch.zeros(2, **f64)
         # theta at the start of the latest replay = the last accepted parameters (a rejected
         # step is undone by the caller before the next replay): off_policy_optimization copies
@@ -321,6 +323,7 @@ class DeviceIteration:
         W1, b1, W2, b2, Wm, bm, ls = self.named
         nt, T, N, k = self.nt, self.T, self.N, self.k
         lt = self.logp.view(nt, T)
+        self._scal_in()
         torch._foreach_copy_(self.shadow, self.params)
         # dH/dlogp at theta_t (loss.backward, mepol.py:273-278) from the importance weights and
         # dH/dW that the previous replay (or _prime) left for logp(theta_t)
@@ -344,6 +347,15 @@ class DeviceIteration:
                                          self.B, self.eps, g_out=self.g_cur)
         torch.cat((self.out_cur[:1], out2[1:2]), out=self.vals)
         self.out_cur.copy_(out2)
+        self._vals_out()
+
+    # The replay's scalar inputs (enable flag, lr and bias corrections) come from, and its two
+    # control outputs go to, pinned host buffers through memcpy nodes of the graph itself.
+    def _scal_in(self):
+        ops.memcpy_async(self.scal, self.scal_host)
+
+    def _vals_out(self):
+        ops.memcpy_async(self.vals_host, self.vals)
 
     @torch.no_grad()
     def _prime(self):
@@ -366,11 +378,14 @@ class DeviceIteration:
         """One eager pass on a side stream (allocator pools, library handles, kernel code)."""
         cur = torch.cuda.current_stream()
         self._side = torch.cuda.Stream(device=self.device)
-        self.scal.zero_()  # enable = 0: the warm-up pass leaves theta and the moments untouched
+        self.scal_np[:] = 0.0  # enable = 0: the warm-up pass leaves theta and the moments alone
         self._side.wait_stream(cur)
         with torch.cuda.stream(self._side):
             self._body()
         cur.wait_stream(self._side)
+        # the pass read the pinned scalar block asynchronously: it must have done so before
+        # the host writes the first real step's values into it
+        self._side.synchronize()
 
     def _capture_graph(self):
         cur = torch.cuda.current_stream()
@@ -392,11 +407,10 @@ class DeviceIteration:
             self.graph = None
         if self.graph is None:
             self._capture()
-        self._advance_scalars()
-        self.scal.copy_(self.scal_host, non_blocking=True)
+        self._advance_scalars()  # into the pinned block the graph copies in
         self.graph.replay()
-        v = self.vals.cpu()
-        return float(v[0]), float(v[1])
+        torch.cuda.current_stream().synchronize()
+        return float(self.vals_np[0]), float(self.vals_np[1])
 
 
 def _row_chunks(n):

@@ -403,5 +403,13 @@ def rollout_mlp(env_id, W1, b1, W2, b2, Wm, bm, log_std, init, noise, states_rec
          _stream())
 
 
+def memcpy_async(dst, src):
+    """dst <- src (same byte size; device or pinned host tensors), ordered on the current
+    stream; inside a graph capture this is a memcpy node."""
+    nbytes = src.numel() * src.element_size()
+    assert dst.numel() * dst.element_size() == nbytes and dst.is_contiguous() and src.is_contiguous()
+    call("mepol_memcpy_async", ptr(dst), ptr(src), nbytes, _stream())
+
+
 def volume_constant(ns, G):
     return math.pi ** (ns / 2) / G

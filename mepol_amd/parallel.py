@@ -305,6 +305,7 @@ class ShardedIteration(DeviceIteration):
 
     @torch.no_grad()
     def _body(self):
+        self._scal_in()
         ep, ops = self.ep, self.ep.ops
         W1, b1, W2, b2, Wm, bm, ls = self.named
         nt, T, k = self.nt, self.T, self.k
@@ -339,6 +340,7 @@ class ShardedIteration(DeviceIteration):
         H = -sums_h[0] + self.B
         KL = sums_k[1] / self.N_global
         torch.stack((H, KL), out=self.vals)
+        self._vals_out()
 
     def try_capture(self):
         """Capture the iteration; all ranks agree on graph or eager.  The warm-up pass issues
