@@ -356,6 +356,9 @@ def run(args):
         gbps = traffic / (knn_ms * 1e-3) / 1e9
         line["roofline"]["hbm_GBps"] = round(gbps, 1)
         line["roofline"]["hbm_frac"] = round(gbps / PEAK_HBM_GBPS, 4)
+    mlp = _mlp_roofline(it) if (it is not None and not sharded) else None
+    if mlp:
+        line["roofline_iteration"] = mlp
     if rollout:
         line["rollout_ms"] = round(roll_ms, 3)
         line["rollout_us_per_step"] = round(roll_ms * 1e3 / T, 2)
@@ -368,6 +371,53 @@ def run(args):
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+PEAK_F64_TFLOPS = 78.6            # MI355X spec: FP64 matrix (dense)
+MEASURED_F64_MFMA_TFLOPS = 49.6   # tools/f64_rate_probe.hip: v_mfma_f64_16x16x4, 8 chains
+
+
+def _mlp_roofline(it):
+    """The iteration's two MFMA kernels timed on their own after the timed region (inside the
+    replayed graph they cannot be event-timed): the fused forward (csrc/policy_fwd.hip) and the
+    fused dh1 GEMM + layer-1 backward (csrc/gemm.hip), on the device iteration's own buffers."""
+    import torch
+
+    from mepol_amd import ops
+
+    if not getattr(it, "fused_fwd", False) or not getattr(it, "fused_dh1", False):
+        return None
+    W1, b1, W2, b2, Wm, bm, ls = it.named
+    N, F = it.x.shape
+    h0, h1w = W1.shape[0], W2.shape[0]
+    dz2 = torch.randn(N, h1w, dtype=torch.float64, device=it.x.device)
+    W2t = W2.detach().t().contiguous()
+    reps = 5
+
+    def timed(fn):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps * 1e-3
+
+    with torch.no_grad():
+        t_f = timed(lambda: ops.policy_forward(it.x, W1, b1, W2, b2, Wm, bm, ls, it.act, it.h1,
+                                               it.z2, it.mu, it.logp))
+        t_b = timed(lambda: ops.dh1_layer1_backward(dz2, W2t, it.h1, it.x, ws=it.ws_dh1))
+    fl_f = 2.0 * N * (h0 * h1w + F * h0)
+    fl_b = 2.0 * N * (h1w * h0 + h0 * (F + 1))
+    out = {"bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_F64_TFLOPS,
+           "measured_f64_mfma_ceiling": MEASURED_F64_MFMA_TFLOPS, "traffic": None,
+           "note": "f64 MFMA kernels of the off-policy iteration, each timed alone with HIP "
+                   "events after the timed region; achieved = algorithmic flops / time"}
+    for key, t, fl in (("policy_forward", t_f, fl_f), ("dh1_layer1_backward", t_b, fl_b)):
+        out[key] = {"us": round(t * 1e6, 1), "achieved": round(fl / t / 1e12, 2),
+                    "frac": round(fl / t / 1e12 / PEAK_F64_TFLOPS, 4)}
+    return out
 
 
 # ---------------------------------------------------------------------------------------------
