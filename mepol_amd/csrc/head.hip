@@ -457,33 +457,59 @@ __global__ __launch_bounds__(512) void head_bwd_wide_kernel(
 
 // out = sum_b part[b][:] in a fixed order: 64 elements per block, wave w sums a quarter of the
 // partials, the 4 quarter sums are added in order.  dW goes to dWm, the tail to dbm / dls.
+// Sum of the per-block partial records in two fixed-order stages (one block column per 64
+// elements with all records serial per wave was latency-bound, 35 us at C3): stage 1 sums
+// record group g (kRedGroups strided groups) for 64 elements per block, stage 2 sums the groups
+// in order and scatters into dWm | dbm | dls | dbz.
+constexpr int kRedGroups = 8;
+
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const double* __restrict__ part,
-                                                              int nblocks, int64_t m, int AH,
-                                                              int A, double* __restrict__ dWm,
-                                                              double* __restrict__ dbm,
-                                                              double* __restrict__ dls,
-                                                              double* __restrict__ dbz) {
+                                                              int nblocks, int64_t m,
+                                                              double* __restrict__ grp) {
   __shared__ double sh[4][64];
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t e = (int64_t)blockIdx.x * 64 + l;
-  const int q = (nblocks + 3) / 4;
-  const int b0 = w * q, b1 = min(nblocks, b0 + q);
+  const int gi = blockIdx.y;
   double s = 0.0;
   if (e < m)
-    for (int b = b0; b < b1; ++b) s += part[(int64_t)b * m + e];
+    for (int b = gi + kRedGroups * w; b < nblocks; b += 4 * kRedGroups)
+      s += part[(int64_t)b * m + e];
   sh[w][l] = s;
   __syncthreads();
-  if (w == 0 && e < m) {
-    const double t = ((sh[0][l] + sh[1][l]) + sh[2][l]) + sh[3][l];
-    if (e < AH)
-      dWm[e] = t;
-    else if (e < AH + A)
-      dbm[e - AH] = t;
-    else if (e < AH + 2 * A)
-      dls[e - AH - A] = t;
-    else if (dbz)
-      dbz[e - AH - 2 * A] = t;
-  }
+  if (w == 0 && e < m) grp[(int64_t)gi * m + e] = ((sh[0][l] + sh[1][l]) + sh[2][l]) + sh[3][l];
+}
+
+__global__ __launch_bounds__(256) void reduce_groups_kernel(const double* __restrict__ grp,
+                                                            int64_t m, int AH, int A,
+                                                            double* __restrict__ dWm,
+                                                            double* __restrict__ dbm,
+                                                            double* __restrict__ dls,
+                                                            double* __restrict__ dbz) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= m) return;
+  double t = 0.0;
+#pragma unroll
+  for (int g = 0; g < kRedGroups; ++g) t += grp[(int64_t)g * m + e];
+  if (e < AH)
+    dWm[e] = t;
+  else if (e < AH + A)
+    dbm[e - AH] = t;
+  else if (e < AH + 2 * A)
+    dls[e - AH - A] = t;
+  else if (dbz)
+    dbz[e - AH - 2 * A] = t;
+}
+
+static int reduce_records(const double* part, int nb, int64_t m, int AH, int A, double* dWm,
+                          double* dbm, double* dls, double* dbz, hipStream_t st) {
+  double* grp = const_cast<double*>(part) + (size_t)nb * m;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((unsigned)((m + 63) / 64), kRedGroups),
+                     dim3(256), 0, st, part, nb, m, grp);
+  MEPOL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(reduce_groups_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st,
+                     grp, m, AH, A, dWm, dbm, dls, dbz);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
 }
 
 static int grid_bwd(int64_t N) {
@@ -534,7 +560,7 @@ extern "C" int mepol_head_forward(const double* z, int64_t n, int hidden, const 
 extern "C" int mepol_head_workspace_size(int64_t n, int hidden, int a_dim, size_t* bytes) {
   if (!bytes || hidden <= 0 || a_dim <= 0) return kErrBadArg;
   const int nb = grid_bwd(std::max<int64_t>(n, 1));
-  *bytes = (size_t)nb * ((size_t)a_dim * (hidden + 2) + hidden) * sizeof(double);
+  *bytes = ((size_t)nb + kRedGroups) * ((size_t)a_dim * (hidden + 2) + hidden) * sizeof(double);
   return 0;
 }
 
@@ -552,7 +578,8 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
     return kErrBadArg;
   }
   const int nb = grid_bwd(n);
-  const size_t need = (size_t)nb * ((size_t)a_dim * (hidden + 2) + hidden) * sizeof(double);
+  const size_t need =
+      ((size_t)nb + kRedGroups) * ((size_t)a_dim * (hidden + 2) + hidden) * sizeof(double);
   if (workspace_bytes < need) {
     set_error("mepol_head_backward: workspace %zu < %zu", workspace_bytes, need);
     return kErrWorkspace;
@@ -579,10 +606,7 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
 #undef MEPOL_HEAD_BWDW
     MEPOL_CHECK_LAUNCH();
     const int64_t m = (int64_t)a_dim * hidden + 2 * a_dim + hidden;
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st,
-                       pdW, nb, m, a_dim * hidden, a_dim, dWm, dbm, dlog_std, dbz);
-    MEPOL_CHECK_LAUNCH();
-    return 0;
+    return reduce_records(pdW, nb, m, a_dim * hidden, a_dim, dWm, dbm, dlog_std, dbz, st);
   }
   const int nc = (hidden + 63) / 64;
   const int ap = a_dim <= 1 ? 1 : a_dim <= 2 ? 2 : a_dim <= 4 ? 4 : 8;
@@ -599,8 +623,5 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
 #undef MEPOL_HEAD_BWD
   MEPOL_CHECK_LAUNCH();
   const int64_t m = (int64_t)a_dim * hidden + 2 * a_dim + hidden;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st, pdW,
-                     nb, m, a_dim * hidden, a_dim, dWm, dbm, dlog_std, dbz);
-  MEPOL_CHECK_LAUNCH();
-  return 0;
+  return reduce_records(pdW, nb, m, a_dim * hidden, a_dim, dWm, dbm, dlog_std, dbz, st);
 }
