@@ -121,17 +121,21 @@ class DeviceIteration:
         self.fused_dh1 = (ops.dh1_layer1_ok(self.x.shape[1], W2.shape[0]) and not self.dh1_first
                           and os.environ.get("MEPOL_FUSED_DH1", "1") != "0")
         self.neg_one = torch.full((), -1.0, **f64)
-        self.scal = torch.zeros(8, **f64)
-        self.scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
-        self.scal_np = self.scal_host.numpy()
-        self.vals_host = torch.zeros(2, dtype=torch.float64).pin_memory()
-        self.vals_np = self.vals_host.numpy()
-        self.vals = torch.zeros(2, **f64)
-        # theta at the start of the latest replay = the last accepted parameters (a rejected
-        # step is undone by the caller before the next replay): off_policy_optimization copies
-        # it into last_valid only when it needs it, not after every accepted step
-        self.shadow = [torch.empty_like(p) for p in self.params]
         self.tracks_shadow = type(self)._body is DeviceIteration._body
+        # Speculative replay (this class's body only): replay t+1 is launched before the host
+        # has read replay t's two scalars, so the GPU never idles on the host's accept/reject
+        # decision.  Two captured graphs alternate; each owns its scalar in/out blocks, its
+        # shadow of theta and a snapshot of the optimizer moments taken before its step, so a
+        # speculative replay can be undone (cancel) when replay t turns out rejected.
+        self.speculative = (self.tracks_shadow
+                            and os.environ.get("MEPOL_SPECULATE", "1") != "0")
+        self._bufs = [self._make_bufs(dev) for _ in range(2 if self.speculative else 1)]
+        self._use(0)
+        self._inflight = []   # parities launched and not yet returned by step(), oldest first
+        self._next = 0
+        self._last = 0        # parity of the replay step() returned last
+        self._events = [torch.cuda.Event() for _ in self._bufs]
+        self.graphs = [None] * len(self._bufs)
         self.w_cur = torch.zeros(self.N, **f64)   # importance weights of logp(theta_t)
         self.g_cur = torch.zeros(self.N, **f64)   # dH/dW at theta_t
         self.out_cur = torch.zeros(4, **f64)      # entropy_forward sums at theta_t
@@ -158,6 +162,40 @@ class DeviceIteration:
                 and [p.data_ptr() for p in target_policy.parameters()]
                 == [p.data_ptr() for p in self.params])
 
+    def _make_bufs(self, dev):
+        f64 = dict(dtype=torch.float64, device=dev)
+        scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
+        vals_host = torch.zeros(2, dtype=torch.float64).pin_memory()
+        # shadow: theta at the start of the replay = the last accepted parameters (a rejected
+        # step is undone by the caller before the next one): off_policy_optimization copies it
+        # into last_valid only when it needs it, not after every accepted step
+        return dict(scal=torch.zeros(8, **f64), scal_host=scal_host, scal_np=scal_host.numpy(),
+                    vals=torch.zeros(2, **f64), vals_host=vals_host, vals_np=vals_host.numpy(),
+                    shadow=[torch.empty_like(p) for p in self.params], moments=[])
+
+    def _use(self, par):
+        """Point the body's scalar blocks / shadows at replay buffer set `par`."""
+        b = self._bufs[par]
+        self.scal, self.scal_host, self.scal_np = b["scal"], b["scal_host"], b["scal_np"]
+        self.vals, self.vals_host, self.vals_np = b["vals"], b["vals_host"], b["vals_np"]
+        self.shadow = b["shadow"]
+        self._moments = b["moments"]
+
+    @property
+    def graph(self):
+        return self.graphs[0]
+
+    @graph.setter
+    def graph(self, g):
+        if g is None:
+            self.graphs = [None] * len(self._bufs)
+        else:
+            self.graphs[0] = g
+
+    def step_start_params(self):
+        """theta at the start of the replay step() returned last (the last accepted one)."""
+        return self._bufs[self._last]["shadow"]
+
     # -- optimizer state (kept in the torch optimizer, as torch.optim would) ------------------
     def _init_state(self):
         for p in self.params:
@@ -178,6 +216,8 @@ class DeviceIteration:
         for t in (self.m or []) + self.v:
             if t.dtype != torch.float64 or not t.is_contiguous() or t.device != self.device:
                 raise ValueError("optimizer state is not contiguous f64 on the policy's device")
+        for b in self._bufs:
+            b["moments"][:] = [torch.empty_like(t) for t in (self.m or []) + self.v]
 
     def _state_tensors_current(self):
         st = self.opt.state
@@ -325,6 +365,8 @@ class DeviceIteration:
         lt = self.logp.view(nt, T)
         self._scal_in()
         torch._foreach_copy_(self.shadow, self.params)
+        if self.speculative:  # the moments before this replay's step (cancel restores them)
+            torch._foreach_copy_(self._moments, (self.m or []) + self.v)
         # dH/dlogp at theta_t (loss.backward, mepol.py:273-278) from the importance weights and
         # dH/dW that the previous replay (or _prime) left for logp(theta_t)
         w, g = self.w_cur, self.g_cur
@@ -389,28 +431,64 @@ class DeviceIteration:
 
     def _capture_graph(self):
         cur = torch.cuda.current_stream()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=self._side):
-            self._body()
+        graphs = []
+        for par in range(len(self._bufs)):
+            self._use(par)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=self._side):
+                self._body()
+            graphs.append(graph)
         cur.wait_stream(self._side)
-        self.graph = graph
+        self._use(0)
+        self.graphs = graphs
 
     def _capture(self):
         self._warmup()
         self._capture_graph()
 
-    def step(self):
-        """policy_update + compute_kl.  Returns host floats (H(theta_t), KL(theta_t+1)
-        unclamped); the target policy's parameters and the optimizer state are updated."""
-        if not self._state_tensors_current():
-            self._init_state()
-            self.graph = None
-        if self.graph is None:
-            self._capture()
+    def _launch(self):
+        par = self._next
+        self._use(par)
         self._advance_scalars()  # into the pinned block the graph copies in
-        self.graph.replay()
-        torch.cuda.current_stream().synchronize()
-        return float(self.vals_np[0]), float(self.vals_np[1])
+        self.graphs[par].replay()
+        self._events[par].record()
+        self._inflight.append(par)
+        self._next = (par + 1) % len(self._bufs)
+
+    def step(self, speculate=False):
+        """policy_update + compute_kl.  Returns host floats (H(theta_t), KL(theta_t+1)
+        unclamped); the target policy's parameters and the optimizer state are updated.
+
+        speculate=True: the caller will run another step if this one is accepted, so that
+        step is launched now, before this one's scalars are read; the next step() returns
+        its results.  If this step is rejected instead, the caller must cancel() first."""
+        if not self._inflight:
+            if not self._state_tensors_current():
+                self._init_state()
+                self.graph = None
+            if self.graph is None:
+                self._capture()
+            self._launch()
+        par = self._inflight.pop(0)
+        if speculate and self.speculative and not self._inflight:
+            self._launch()
+        self._events[par].synchronize()
+        self._last = par
+        v = self._bufs[par]["vals_np"]
+        return float(v[0]), float(v[1])
+
+    @torch.no_grad()
+    def cancel(self):
+        """Undo a speculative replay still in flight: wait for it and restore theta, the
+        optimizer moments and the step count it advanced (as they were after the rejected
+        step; the caller then restores the last accepted theta from step_start_params())."""
+        while self._inflight:
+            par = self._inflight.pop()
+            self._events[par].synchronize()
+            torch._foreach_copy_((self.m or []) + self.v, self._bufs[par]["moments"])
+            torch._foreach_copy_(self.params, self._bufs[par]["shadow"])
+            torch._foreach_add_([self.opt.state[p]["step"] for p in self.params], -1.0)
+            self._next = par
 
 
 def _row_chunks(n):

@@ -760,12 +760,17 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
             loop.refresh()
     # device loop: the parameters before each replay's step are kept on the device (the last
     # accepted ones), so last_valid is only written when a step is rejected and at the end
-    shadow = loop.shadow if loop is not None and getattr(loop, "tracks_shadow", False) else None
+    shadow = loop is not None and getattr(loop, "tracks_shadow", False)
     last_accepted = False
     while not kl_threshold_reached:
         if loop is not None:
-            # policy_update + compute_kl as one graph replay; two scalars come back
-            H, KL = loop.step()
+            # policy_update + compute_kl as one graph replay; two scalars come back.  When an
+            # accepted step would be followed by another one, that next replay is launched
+            # before this one's scalars are read (the GPU does not wait for the host's
+            # decision); a rejection cancels it (optimizer moments and step count restored).
+            more = (not (use_backtracking and backtrack_iter > 1)
+                    and num_off_iters + 1 != max_off_iters)
+            H, KL = loop.step(speculate=more) if shadow else loop.step()
             loss, numeric_error, kl, kl_numeric_error = device_loop.kl_flags(H, KL)
             entropy = -loss
         elif deferred:
@@ -792,7 +797,7 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
             kl = _np(kl)
 
         if not numeric_error and not kl_numeric_error and kl <= kl_threshold:
-            if shadow is None:
+            if not shadow:
                 _copy_policy(last_valid_target_policy, target_policy)
             last_accepted = True
             num_off_iters += 1
@@ -800,8 +805,9 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
                 on_accept(num_off_iters, entropy, kl, learning_rate)
         else:
             last_accepted = False
-            if shadow is not None:
-                _copy_params(last_valid_target_policy, shadow)
+            if shadow:
+                loop.cancel()
+                _copy_params(last_valid_target_policy, loop.step_start_params())
             if use_backtracking:
                 if not backtrack_iter == max_backtrack_try:
                     _copy_policy(target_policy, last_valid_target_policy)
@@ -819,8 +825,10 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
         if num_off_iters == max_off_iters:
             kl_threshold_reached = True
 
-    if shadow is not None and last_accepted:
-        _copy_policy(last_valid_target_policy, target_policy)
+    if shadow:
+        loop.cancel()  # nothing is in flight here; kept as a guard
+        if last_accepted:
+            _copy_policy(last_valid_target_policy, target_policy)
     with torch.no_grad():
         entropy = fns.compute_entropy(last_valid_target_policy, last_valid_target_policy, states,
                                       actions, num_traj, real_traj_lengths, distances, indices, k,

@@ -46,7 +46,8 @@ def _setup(opt_name, lr, seed=5, cfg=None):
     return M, (states, actions), beh, tgt, last, opt, batch
 
 
-def _run(monkeypatch, graph, opt_name, lr, kl_threshold, max_off_iters=6, cfg=None):
+def _run(monkeypatch, graph, opt_name, lr, kl_threshold, max_off_iters=6, cfg=None,
+         backtracking=True):
     from mepol_amd.algorithms import device_loop
 
     c = cfg or SMALL
@@ -58,13 +59,34 @@ def _run(monkeypatch, graph, opt_name, lr, kl_threshold, max_off_iters=6, cfg=No
     trace = []
     res = M.off_policy_optimization(
         opt, beh, tgt, last, st, ac, NT, rl, D, I, K, G, B, NF, 0.0, kl_threshold, max_off_iters,
-        True, 2, 4, lr, on_accept=lambda n, e, kl, l: trace.append((n, float(e), float(kl), l)))
+        backtracking, 2, 4, lr,
+        on_accept=lambda n, e, kl, l: trace.append((n, float(e), float(kl), l)))
     used = tgt in device_loop._CACHE
     params = torch.cat([p.detach().reshape(-1) for p in last.parameters()]).cpu().numpy()
     state = opt.state_dict()["state"]
     steps = [float(state[i]["step"]) for i in sorted(state)]
+    moments = np.concatenate([state[i][key].detach().reshape(-1).cpu().numpy()
+                              for i in sorted(state) for key in sorted(state[i])
+                              if key != "step"])
+    tparams = torch.cat([p.detach().reshape(-1) for p in tgt.parameters()]).cpu().numpy()
     return dict(H=float(res[0]), n=res[1], bt=res[2], lr=res[3], trace=trace, params=params,
-                steps=steps, used=used, raw=raw, D=D, I=I)
+                steps=steps, used=used, raw=raw, D=D, I=I, moments=moments, tparams=tparams)
+
+
+def _assert_same_run(g, e):
+    assert g["used"] and not e["used"]
+    assert (g["n"], g["bt"], g["lr"]) == (e["n"], e["bt"], e["lr"])
+    assert g["steps"] == e["steps"]
+    assert len(g["trace"]) == len(e["trace"])
+    for a, b in zip(g["trace"], e["trace"]):
+        assert a[0] == b[0] and a[3] == b[3]
+        np.testing.assert_allclose(a[1:3], b[1:3], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(g["H"], e["H"], rtol=1e-9)
+    np.testing.assert_allclose(g["params"], e["params"], rtol=1e-8, atol=1e-11)
+    np.testing.assert_allclose(g["tparams"], e["tparams"], rtol=1e-8, atol=1e-11)
+    # the optimizer moments carry into the next epoch: a cancelled speculative replay must
+    # leave them exactly as the rejected step did
+    np.testing.assert_allclose(g["moments"], e["moments"], rtol=1e-8, atol=1e-14)
 
 
 @pytest.mark.parametrize("opt_name,lr,kl_threshold,cfg", [
@@ -79,15 +101,28 @@ def test_graph_loop_matches_eager(cuda, monkeypatch, opt_name, lr, kl_threshold,
         monkeypatch.setenv("MEPOL_ITER_CHUNKS", "4")
     g = _run(monkeypatch, True, opt_name, lr, kl_threshold, cfg=cfg)
     e = _run(monkeypatch, False, opt_name, lr, kl_threshold, cfg=cfg)
-    assert g["used"] and not e["used"]
-    assert (g["n"], g["bt"], g["lr"]) == (e["n"], e["bt"], e["lr"])
-    assert g["steps"] == e["steps"]
-    assert len(g["trace"]) == len(e["trace"])
-    for a, b in zip(g["trace"], e["trace"]):
-        assert a[0] == b[0] and a[3] == b[3]
-        np.testing.assert_allclose(a[1:3], b[1:3], rtol=1e-9, atol=1e-12)
-    np.testing.assert_allclose(g["H"], e["H"], rtol=1e-9)
-    np.testing.assert_allclose(g["params"], e["params"], rtol=1e-8, atol=1e-11)
+    _assert_same_run(g, e)
+
+
+@pytest.mark.parametrize("backtracking", [True, False])
+@pytest.mark.parametrize("speculate", ["1", "0"])
+def test_graph_loop_mid_loop_rejection(cuda, monkeypatch, backtracking, speculate):
+    """A step rejected after accepted ones, while the next replay is already in flight
+    (speculative launch): the cancelled replay leaves theta, the moments and the step count
+    as the eager loop does, with and without backtracking."""
+    monkeypatch.setenv("MEPOL_SPECULATE", speculate)
+    probe = _run(monkeypatch, False, "adam", 1e-3, 1e9, max_off_iters=6)
+    kls = [t[2] for t in probe["trace"]]
+    # the last step whose KL exceeds every earlier one: a threshold between them accepts the
+    # steps before it and rejects it (KL is not monotone in the step count)
+    cut = [i for i in range(1, len(kls)) if kls[i] > max(kls[:i])]
+    assert len(kls) == 6 and cut, kls
+    i = cut[-1]
+    thr = 0.5 * (max(kls[:i]) + kls[i])
+    g = _run(monkeypatch, True, "adam", 1e-3, thr, max_off_iters=6, backtracking=backtracking)
+    e = _run(monkeypatch, False, "adam", 1e-3, thr, max_off_iters=6, backtracking=backtracking)
+    assert i <= e["n"] <= i + int(backtracking)  # + the backtracked step, if accepted
+    _assert_same_run(g, e)
 
 
 @pytest.mark.parametrize("cfg,lr", [(SMALL, 1e-3), (C3, 1e-4), (C4, 1e-4), (C5, 1e-4)],
