@@ -200,6 +200,16 @@ int mepol_rollout_step(int env_id, double* env_f64, float* env_f32, const double
 int mepol_optim_step(int kind, int n_tensors, double* const* params, const double* const* grads,
                      double* const* exp_avg, double* const* exp_avg_sq, const int64_t* sizes,
                      const double* scalars, void* stream);
+/* mepol_optim_step that also writes each tensor's values from before the update into
+ * params_snap / exp_avg_snap / exp_avg_sq_snap (arrays of n_tensors device pointers, each array
+ * may be NULL): the device iteration's shadow of the last accepted theta and its optimizer-moment
+ * snapshot (algorithms/device_loop.py, mepol.py:441-456 semantics). */
+int mepol_optim_step_snapshot(int kind, int n_tensors, double* const* params,
+                              const double* const* grads, double* const* exp_avg,
+                              double* const* exp_avg_sq, const int64_t* sizes,
+                              const double* scalars, double* const* params_snap,
+                              double* const* exp_avg_snap, double* const* exp_avg_sq_snap,
+                              void* stream);
 
 #ifdef __cplusplus
 }

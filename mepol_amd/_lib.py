@@ -67,6 +67,8 @@ SIGNATURES = {
                           _c_vp],
     "mepol_memcpy_async": [_c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_optim_step": [_c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
+    "mepol_optim_step_snapshot": [_c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                  _c_vp, _c_vp, _c_vp, _c_vp],
 }
 _RESTYPES = {"mepol_last_error_string": ctypes.c_char_p}
 

@@ -364,9 +364,6 @@ class DeviceIteration:
         nt, T, N, k = self.nt, self.T, self.N, self.k
         lt = self.logp.view(nt, T)
         self._scal_in()
-        torch._foreach_copy_(self.shadow, self.params)
-        if self.speculative:  # the moments before this replay's step (cancel restores them)
-            torch._foreach_copy_(self._moments, (self.m or []) + self.v)
         # dH/dlogp at theta_t (loss.backward, mepol.py:273-278) from the importance weights and
         # dH/dW that the previous replay (or _prime) left for logp(theta_t)
         w, g = self.w_cur, self.g_cur
@@ -377,8 +374,13 @@ class DeviceIteration:
         dW1, db1, dW2, db2, dWm, dbm, dls = self._backward(grad.view(-1))
         # optimizer.step() (mepol.py:280)
         grad_of = {id(p): g for p, g in zip(self.named, (dW1, db1, dW2, db2, dWm, dbm, dls))}
+        # the step also leaves theta_t in the shadow and, speculative, the moments before it
+        # (cancel restores them), without separate copy launches
+        nm = len(self.m) if self.m is not None else 0
+        snap = (self.shadow, self._moments[:nm] if (self.speculative and nm) else None,
+                self._moments[nm:] if self.speculative else None)
         ops.optim_step(self.kind, self.params, [grad_of[id(p)] for p in self.params], self.m,
-                       self.v, self.scal)
+                       self.v, self.scal, snapshot=snap)
         # compute_kl at theta_t+1 (mepol.py:435, :157-174).  The pass with the entropy
         # constants also yields the KL sum (its terms do not depend on them) and the next
         # iteration's H(theta_t+1) and dH/dW, so each replay needs one weights pass, not two.

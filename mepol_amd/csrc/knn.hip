@@ -773,11 +773,27 @@ __device__ __forceinline__ bool lex_less_f(float a, int ai, float b, int bi) {
 
 // Exact f64 squared distance, summed in feature order with no contraction (matches the
 // reference's kd_tree rdist: sum of (x_f - y_f)^2 in double, f = 0..d-1).
+// The row is read 32 features at a time with every load issued before the first use (clamped,
+// unconditional addresses): one memory latency per chunk instead of one per feature (the
+// refine's random candidate rows miss L2, and the per-feature loop serialised those misses).
 __device__ __forceinline__ double exact_d2(const float* __restrict__ a, const float* __restrict__ b, int d) {
+  constexpr int kCh = 32;
   double s = 0.0;
-  for (int f = 0; f < d; ++f) {
-    const double t = __dsub_rn((double)a[f], (double)b[f]);
-    s = __dadd_rn(s, __dmul_rn(t, t));
+  for (int f0 = 0; f0 < d; f0 += kCh) {
+    float av[kCh], bv[kCh];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      const int f = min(f0 + u, d - 1);
+      av[u] = a[f];
+      bv[u] = b[f];
+    }
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      if (f0 + u < d) {  // uniform condition
+        const double t = __dsub_rn((double)av[u], (double)bv[u]);
+        s = __dadd_rn(s, __dmul_rn(t, t));
+      }
+    }
   }
   return s;
 }
@@ -804,11 +820,21 @@ __global__ __launch_bounds__(256) void refine_kernel(
     const unsigned* __restrict__ cmax_bits, int e_terms, const float* __restrict__ tau,
     double* __restrict__ Dout,
     int64_t* __restrict__ I64, int32_t* __restrict__ I32, int* __restrict__ flag_count,
-    int* __restrict__ flag_list) {
+    int* __restrict__ flag_list, int rank_merge) {
   __shared__ int sel[4][64];
+  constexpr int kRM = MAXP <= 4 ? MAXP : 1;  // rank merge for M <= 256 entries
+  __shared__ float2 sent[4][64 * kRM];        // rank merge: the query's entries (value, index bits)
+  if (MAXP > 4) rank_merge = 0;
   const int w = threadIdx.x >> 6;
   const int l = threadIdx.x & 63;
-  const int64_t q = (int64_t)blockIdx.x * 4 + w;
+  // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs, so block b runs on
+  // XCD b % 8; each XCD gets one contiguous range of query blocks.  Neighbouring queries' rows of
+  // the transposed index table (I32[l][q], 4 bytes per query) then meet in one L2 and leave it
+  // as whole lines instead of 16-byte pieces from 8 different L2s.
+  const int64_t nb = gridDim.x, bx = blockIdx.x;
+  const int64_t xcd = bx & 7, per = nb >> 3, rem = nb & 7;
+  const int64_t qb = xcd * per + min(xcd, rem) + (bx >> 3);
+  const int64_t q = qb * 4 + w;
   if (q >= nq) return;
   // Candidate entries of this query: M per query.  Lists mode (counts == nullptr): 2*split
   // ascending partial lists of list_len each.  Survivor mode: counts[q] unsorted entries (a count
@@ -845,10 +871,45 @@ __global__ __launch_bounds__(256) void refine_kernel(
     ev[p] = v;
     ei[p] = ix;
   }
-  // LIST rounds of wave argmin over (approx, idx): approximate top-LIST of the union.
+  // Approximate top-LIST of the union, ordered by (approx, idx).
   float last = INFINITY;
+  if (rank_merge) {
+    // Rank merge: every entry's rank = the number of entries lexicographically below it,
+    // counted against all M entries read back from LDS (broadcast reads, no dependent chain);
+    // entries of rank < LIST land in sel[rank].  Same selection as the argmin rounds below.
+#pragma unroll
+    for (int p = 0; p < kRM; ++p)
+      sent[w][p * 64 + l] = make_float2(ev[p], __int_as_float(ei[p]));
+    if (l < LIST) sel[w][l] = -1;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    int rk[MAXP];
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p) rk[p] = 0;
+    const int mtot = min(nval, 64 * kRM);
 #pragma nounroll
-  for (int r = 0; r < LIST; ++r) {
+    for (int e = 0; e < mtot; ++e) {
+      const float2 o = sent[w][e];
+      const float ov = o.x;
+      const int oi = __float_as_int(o.y);
+#pragma unroll
+      for (int p = 0; p < MAXP; ++p) rk[p] += lex_less_f(ov, oi, ev[p], ei[p]) ? 1 : 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int p = 0; p < MAXP; ++p) {
+      if (ei[p] != INT_MAX && rk[p] < LIST) {
+        sel[w][rk[p]] = ei[p];
+        if (rk[p] == LIST - 1) sent[w][0].x = ev[p];  // read back below as `last`
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int s_last = sel[w][LIST - 1];
+    last = (s_last >= 0) ? sent[w][0].x : INFINITY;
+  }
+#pragma nounroll
+  for (int r = 0; r < (rank_merge ? 0 : LIST); ++r) {
     float bv = ev[0];
     int bi = ei[0];
 #pragma unroll
@@ -908,8 +969,10 @@ __global__ __launch_bounds__(256) void refine_kernel(
     }
   }
   // Certification: every candidate outside `sel` has exact d^2 >= bnd + |q|^2 - E.
-  double qn2 = 0.0;
-  for (int f = 0; f < d; ++f) qn2 += (double)xq[f] * (double)xq[f];
+  double qn2 = 0.0;  // |q|^2 for the certification bound (any summation order)
+  for (int f = l; f < d; f += 64) qn2 += (double)xq[f] * (double)xq[f];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) qn2 += __shfl_xor(qn2, m, kWave);
   const double cmax = (double)__uint_as_float(*cmax_bits);
   // e_terms * 2^-24 * (C^2 + 2 C |q|) bounds the selection's error (f32 path: 4 (d + 1);
   // split-f16 path: 2 (3 K + 16 + d), see make_plan), C = max candidate norm.
@@ -1255,6 +1318,15 @@ static void launch_select16_ks(const Plan& P, const _Float16* ap, const float* q
 #undef MEPOL_SEL16
 }
 
+// MEPOL_KNN_RANK_MERGE=0 selects the argmin-round merge in refine_kernel (A/B probe).
+static int refine_rank_merge() {
+  static const int v = [] {
+    const char* e = getenv("MEPOL_KNN_RANK_MERGE");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 template <int LIST>
 static void launch_refine_list(const Plan& P, const float* cand, const float* query,
                                const float* lv, const int* li, const unsigned* cmax,
@@ -1264,19 +1336,19 @@ static void launch_refine_list(const Plan& P, const float* cand, const float* qu
   // MAXP = ceil(M / 64) <= 32
   if (P.maxp <= 2)
     hipLaunchKernelGGL((refine_kernel<LIST, 2>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl);
+                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl, refine_rank_merge());
   else if (P.maxp <= 4)
     hipLaunchKernelGGL((refine_kernel<LIST, 4>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl);
+                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl, refine_rank_merge());
   else if (P.maxp <= 8)
     hipLaunchKernelGGL((refine_kernel<LIST, 8>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl);
+                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl, refine_rank_merge());
   else if (P.maxp <= 16)
     hipLaunchKernelGGL((refine_kernel<LIST, 16>), g, dim3(256), 0, st, cand, P.nc, query, P.nq,
-                       P.d, P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl);
+                       P.d, P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl, refine_rank_merge());
   else
     hipLaunchKernelGGL((refine_kernel<LIST, 32>), g, dim3(256), 0, st, cand, P.nc, query, P.nq,
-                       P.d, P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl);
+                       P.d, P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl, refine_rank_merge());
 }
 
 template <int LIST>

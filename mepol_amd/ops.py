@@ -348,21 +348,29 @@ def layer_backward(dh, h, x, ws=None):
     return dW, db
 
 
-def optim_step(kind, params, grads, exp_avg, exp_avg_sq, scalars):
+def optim_step(kind, params, grads, exp_avg, exp_avg_sq, scalars, snapshot=None):
     """In-place Adam (kind 0) / RMSprop (kind 1) update of f64 tensors; scalars is a device f64
-    tensor (see include/mepol_amd.h, mepol_optim_step)."""
+    tensor (see include/mepol_amd.h, mepol_optim_step).  snapshot = (params_snap, exp_avg_snap,
+    exp_avg_sq_snap) lists (entries may be None) receive the values from before the update."""
     import ctypes
 
     n = len(params)
     arr = ctypes.c_void_p * n
-    for t in list(params) + list(grads) + list(exp_avg_sq) + list(exp_avg or []):
+    snaps = list(snapshot) if snapshot is not None else [None, None, None]
+    for t in (list(params) + list(grads) + list(exp_avg_sq) + list(exp_avg or [])
+              + [x for lst in snaps if lst is not None for x in lst]):
         if t.dtype != torch.float64 or not t.is_contiguous() or not t.is_cuda:
             raise ValueError("optim_step needs contiguous f64 device tensors")
+    for lst in snaps:
+        if lst is not None and (len(lst) != n or any(
+                a.numel() != b.numel() for a, b in zip(lst, params))):
+            raise ValueError("optim_step: snapshot tensors must match the parameters")
     sizes = (ctypes.c_int64 * n)(*[t.numel() for t in params])
     m = arr(*[t.data_ptr() for t in exp_avg]) if exp_avg is not None else None
-    call("mepol_optim_step", kind, n, arr(*[t.data_ptr() for t in params]),
+    sp = [arr(*[t.data_ptr() for t in lst]) if lst is not None else None for lst in snaps]
+    call("mepol_optim_step_snapshot", kind, n, arr(*[t.data_ptr() for t in params]),
          arr(*[t.data_ptr() for t in grads]), m, arr(*[t.data_ptr() for t in exp_avg_sq]),
-         sizes, ptr(scalars), _stream())
+         sizes, ptr(scalars), sp[0], sp[1], sp[2], _stream())
 
 
 def step_mountaincar(state, action):
