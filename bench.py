@@ -149,6 +149,31 @@ def selftest(args):
         dist.destroy_process_group()
 
 
+_JSON_FD = None
+
+
+def _quiet_stdout():
+    """Route fd 1 to /dev/null for the rest of the run and keep the real stdout for the one
+    JSON line: RCCL prints its version banner on stdout when a communicator is created, and the
+    contract is a single JSON line from rank 0."""
+    global _JSON_FD
+    if _JSON_FD is None:
+        sys.stdout.flush()
+        _JSON_FD = os.dup(1)
+        null = os.open(os.devnull, os.O_WRONLY)
+        os.dup2(null, 1)
+        os.close(null)
+
+
+def _emit(line):
+    text = json.dumps(line) + "\n"
+    if _JSON_FD is None:
+        print(text, end="", flush=True)
+    else:
+        sys.stdout.flush()
+        os.write(_JSON_FD, text.encode())
+
+
 def run(args):
     import torch
 
@@ -171,6 +196,8 @@ def run(args):
     sharded = world > 1 or os.environ.get("MEPOL_BENCH_SHARDED") == "1"
     if sharded:
         import torch.distributed as dist
+
+        _quiet_stdout()
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
@@ -368,7 +395,7 @@ def run(args):
         line["config"]["rehearsal"] = f"{world} ranks on {torch.cuda.device_count()} GPU(s), gloo"
     if not args.no_cpu_baseline and world == 1:
         line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample_queries, iters_done)
-    print(json.dumps(line), flush=True)
+    _emit(line)
     if dist is not None:
         dist.destroy_process_group()
 

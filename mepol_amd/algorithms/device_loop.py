@@ -121,14 +121,16 @@ class DeviceIteration:
         self.fused_dh1 = (ops.dh1_layer1_ok(self.x.shape[1], W2.shape[0]) and not self.dh1_first
                           and os.environ.get("MEPOL_FUSED_DH1", "1") != "0")
         self.neg_one = torch.full((), -1.0, **f64)
-        self.tracks_shadow = type(self)._body is DeviceIteration._body
-        # Speculative replay (this class's body only): replay t+1 is launched before the host
+        # every body takes its optimizer step through _optim_step, which leaves theta_t in the
+        # replay's shadow (off_policy_optimization then copies it into last_valid only when it
+        # needs it, not after every accepted step)
+        self.tracks_shadow = True
+        # Speculative replay: replay t+1 is launched before the host
         # has read replay t's two scalars, so the GPU never idles on the host's accept/reject
         # decision.  Two captured graphs alternate; each owns its scalar in/out blocks, its
         # shadow of theta and a snapshot of the optimizer moments taken before its step, so a
         # speculative replay can be undone (cancel) when replay t turns out rejected.
-        self.speculative = (self.tracks_shadow
-                            and os.environ.get("MEPOL_SPECULATE", "1") != "0")
+        self.speculative = os.environ.get("MEPOL_SPECULATE", "1") != "0"
         self._bufs = [self._make_bufs(dev) for _ in range(2 if self.speculative else 1)]
         self._use(0)
         self._inflight = []   # parities launched and not yet returned by step(), oldest first
@@ -374,13 +376,7 @@ class DeviceIteration:
         dW1, db1, dW2, db2, dWm, dbm, dls = self._backward(grad.view(-1))
         # optimizer.step() (mepol.py:280)
         grad_of = {id(p): g for p, g in zip(self.named, (dW1, db1, dW2, db2, dWm, dbm, dls))}
-        # the step also leaves theta_t in the shadow and, speculative, the moments before it
-        # (cancel restores them), without separate copy launches
-        nm = len(self.m) if self.m is not None else 0
-        snap = (self.shadow, self._moments[:nm] if (self.speculative and nm) else None,
-                self._moments[nm:] if self.speculative else None)
-        ops.optim_step(self.kind, self.params, [grad_of[id(p)] for p in self.params], self.m,
-                       self.v, self.scal, snapshot=snap)
+        self._optim_step([grad_of[id(p)] for p in self.params])
         # compute_kl at theta_t+1 (mepol.py:435, :157-174).  The pass with the entropy
         # constants also yields the KL sum (its terms do not depend on them) and the next
         # iteration's H(theta_t+1) and dH/dW, so each replay needs one weights pass, not two.
@@ -392,6 +388,15 @@ class DeviceIteration:
         torch.cat((self.out_cur[:1], out2[1:2]), out=self.vals)
         self.out_cur.copy_(out2)
         self._vals_out()
+
+    def _optim_step(self, grads):
+        """optimizer.step() (mepol.py:280).  The kernel also leaves theta_t in the replay's
+        shadow and, when speculative, the moments before the step (cancel restores them),
+        without separate copy launches."""
+        nm = len(self.m) if self.m is not None else 0
+        snap = (self.shadow, self._moments[:nm] if (self.speculative and nm) else None,
+                self._moments[nm:] if self.speculative else None)
+        ops.optim_step(self.kind, self.params, grads, self.m, self.v, self.scal, snapshot=snap)
 
     # The replay's scalar inputs (enable flag, lr and bias corrections) come from, and its two
     # control outputs go to, pinned host buffers through memcpy nodes of the graph itself.

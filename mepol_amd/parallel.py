@@ -330,7 +330,7 @@ class ShardedIteration(DeviceIteration):
         for p in self.params:
             grads.append(flat[o:o + p.numel()].view_as(p))
             o += p.numel()
-        ops.optim_step(self.kind, self.params, grads, self.m, self.v, self.scal)
+        self._optim_step(grads)
         # KL at theta_t+1 (ShardedEpoch.compute_kl)
         self.forward()
         _, w2 = self._weights(lt)
