@@ -418,9 +418,14 @@ class DeviceIteration:
         self.g_cur.copy_(g)
         self.out_cur.copy_(out)
 
-    def refresh(self):
-        """Recompute the iteration's inputs that depend on theta (logp, w, dH/dW)."""
-        self.forward()
+    def refresh(self, logp=None):
+        """Recompute the iteration's inputs that depend on theta (logp, w, dH/dW).  logp: the
+        target's log-probabilities when the caller already has them (the epoch's first step,
+        where the target holds the behavioral parameters)."""
+        if logp is None:
+            self.forward()
+        else:
+            self.logp.copy_(logp.reshape(-1))
         self._prime()
 
     def _warmup(self):

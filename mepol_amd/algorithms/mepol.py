@@ -750,14 +750,18 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
     from . import device_loop
 
     loop = None
+    batch = None
     if deferred and hasattr(fns, "make_device_loop"):
         loop = fns.make_device_loop(optimizer, behavioral_policy, target_policy)
     elif deferred and fns is sys.modules[__name__]:
         batch = P.lookup(states, actions, real_traj_lengths, distances, indices)
         if device_loop.supported(batch, behavioral_policy, target_policy, optimizer):
             loop = device_loop.get(target_policy, optimizer, batch, k, G, B, ns, eps)
-            loop.load(batch, batch.behavioral_logp(behavioral_policy))
-            loop.refresh()
+            logp_b = batch.behavioral_logp(behavioral_policy)
+            loop.load(batch, logp_b)
+            # At an epoch's start the target holds the behavioral parameters (mepol.py:409, 493):
+            # its log-probabilities are then logp_b itself, not another forward pass.
+            loop.refresh(logp=logp_b if _same_params(target_policy, behavioral_policy) else None)
     # device loop: the parameters before each replay's step are kept on the device (the last
     # accepted ones), so last_valid is only written when a step is rejected and at the end
     shadow = loop is not None and getattr(loop, "tracks_shadow", False)
@@ -829,6 +833,10 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
         loop.cancel()  # nothing is in flight here; kept as a guard
         if last_accepted:
             _copy_policy(last_valid_target_policy, target_policy)
+            if batch is not None:
+                # the last replay's forward ran at exactly these parameters: its logp serves
+                # the final entropy's forward of last_valid (mepol.py:466-468)
+                batch.seed_behavioral_logp(last_valid_target_policy, loop.logp)
     with torch.no_grad():
         entropy = fns.compute_entropy(last_valid_target_policy, last_valid_target_policy, states,
                                       actions, num_traj, real_traj_lengths, distances, indices, k,
@@ -837,6 +845,17 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
 
 
 _BUILTIN_STEP_FNS = (policy_update, compute_kl)
+
+
+def _same_params(a, b):
+    """True when two policies hold bitwise equal parameters (one host synchronisation)."""
+    pa, pb = list(a.parameters()), list(b.parameters())
+    if len(pa) != len(pb) or any(x.shape != y.shape or x.dtype != y.dtype for x, y in zip(pa, pb)):
+        return False
+    with torch.no_grad():
+        fa = torch.cat([x.reshape(-1) for x in pa])
+        fb = torch.cat([y.reshape(-1) for y in pb])
+        return bool(torch.equal(fa, fb))
 
 
 def _copy_params(dst, tensors):

@@ -63,6 +63,13 @@ class ParticleBatch:
                 self._logp_b = (key, self.logp(policy).detach())
         return self._logp_b[1]
 
+    def seed_behavioral_logp(self, policy, logp):
+        """Cache `logp` (computed elsewhere at the policy's current parameters) as the policy's
+        behavioral log-probabilities, so behavioral_logp(policy) needs no forward pass."""
+        with torch.no_grad():
+            self._logp_b = (_param_key(policy),
+                            logp.detach().reshape(self.num_traj, self.T).clone())
+
     def csr(self, k):
         if k not in self._csr:
             self._csr[k] = ops.csr_build(self.idx32T, k, self.N)
