@@ -332,8 +332,14 @@ def run(args):
     knn_tflops = F / (knn_ms * 1e-3) / 1e12
     # Which selection the library ran (include/mepol_amd.h; MEPOL_KNN_PRECISION=f32 forces f32):
     # split-f16 issues 3 products x 2 x K flops per (query, candidate), K = 16*ceil((d+1)/16).
-    if os.environ.get("MEPOL_KNN_PRECISION", "") != "f32" and d + 1 <= 48 and k + 1 <= 60:
-        K16 = 16 * ((d + 1 + 15) // 16)
+    # (make_plan in csrc/knn.hip: split-f16 for KS16 <= 3 with lists <= 40 (32 at KS16 = 3),
+    # and KS16 = 4 with lists <= 32)
+    ks16 = (d + 1 + 15) // 16
+    keep = (k + 2) // 2 + 2
+    list16 = next((v for v in (8, 16, 24, 32, 40) if v >= keep + 4), 64)
+    f16_sel = (ks16 <= 3 and list16 <= (32 if ks16 == 3 else 40)) or (ks16 == 4 and list16 <= 32)
+    if os.environ.get("MEPOL_KNN_PRECISION", "") != "f32" and f16_sel:
+        K16 = 16 * ks16
         knn_issued = 3 * 2 * K16 * float(nq) * N
         knn_peak = PEAK_F16_TFLOPS
         knn_desc = "split-f16 MFMA selection (3 products, f32 accumulate) + f64 exact refine (bit-exact output)"

@@ -475,8 +475,11 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
   // read it has completed (its results were consumed).  Loads are inline asm with hand-counted
   // waits (NV per tile; no other vector-memory op in the loop).
   constexpr int NV = 2 * KS16;  // dwordx4 per lane per tile: hi and lo halves of each k-step
+  // Fragment buffers: three for KS16 <= 3; two for KS16 = 4 (d + 1 <= 64, HandReach), whose
+  // 8-register-per-k-step buffers would otherwise put the kernel at the 256-VGPR cap.
+  constexpr int NB = KS16 >= 4 ? 2 : 3;
   const f32x4* abase = reinterpret_cast<const f32x4*>(apack) + (int64_t)l * NV;
-  f32x4 Bf[3][NV];
+  f32x4 Bf[NB][NV];
   auto load = [&](f32x4 (&A)[NV], int64_t t) {
     const f32x4* p = abase + t * tile_stride * 64 * NV;
 #pragma unroll
@@ -526,7 +529,46 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
         flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0, keep);
     }
   };
-  if (t0 < t1) {
+  if constexpr (NB == 2) {
+    if (t0 < t1) {
+      // Double buffer: tile t+1's loads are issued right after tile t's MFMA chain (the chain
+      // of t-1, the last reader of that buffer, executed before chain t in the matrix pipe)
+      // and land while the chain and the threshold work of t-1 run; each step then waits for
+      // all outstanding loads, which are exactly tile t's.
+      const int64_t tl = t1 - 1;
+      load(Bf[0], t0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[0][v]));
+      f32x16 accP = chain(Bf[0]);
+      load(Bf[1], min(t0 + 1, tl));
+      int64_t t = t0 + 1;
+#define MEPOL_SEL16_STEP2(CUR, NXT)                            \
+  {                                                           \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          \
+    _Pragma("unroll") for (int v = 0; v < NV; ++v)            \
+        asm volatile("" : "+v"(Bf[CUR][v]));                  \
+    const f32x16 accN = chain(Bf[CUR]);                       \
+    load(Bf[NXT], min(t + 1, tl));                            \
+    process(accP, t - 1);                                     \
+    accP = accN;                                              \
+    ++t;                                                      \
+  }
+#pragma nounroll
+      while (t + 1 < t1) {
+        MEPOL_SEL16_STEP2(1, 0)
+        MEPOL_SEL16_STEP2(0, 1)
+      }
+      if (t < t1) MEPOL_SEL16_STEP2(1, 0)
+#undef MEPOL_SEL16_STEP2
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[b][v]));
+      process(accP, t - 1);
+    }
+  } else if (t0 < t1) {
     const int64_t tl = t1 - 1;
     load(Bf[0], t0);
     load(Bf[1], min(t0 + 1, tl));
@@ -560,7 +602,7 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
     // dead may be given registers that a later instruction reuses while the data is in flight.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-    for (int b = 0; b < 3; ++b)
+    for (int b = 0; b < NB; ++b)
 #pragma unroll
       for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[b][v]));
     process(accP, t - 1);
@@ -1162,7 +1204,9 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
     // split-f16 instantiations that stay below the 256-VGPR cap (at the cap the fragment
     // buffers of the asm-load pipeline are no longer safe from register copies)
     // (<3, 40> and every KS16 = 4 list size needed for kp1 > 21 reach the cap: excluded)
-    const bool fits = P->KS16 <= 3 && P->LIST16 <= (P->KS16 == 3 ? 32 : 40);
+    // KS16 = 4 runs a double-buffered pipeline (select16_kernel, NB = 2) with lists <= 32
+    const bool fits = (P->KS16 <= 3 && P->LIST16 <= (P->KS16 == 3 ? 32 : 40)) ||
+                      (P->KS16 == 4 && P->LIST16 <= 32);
     P->mode = (!want_f32 && fits) ? 1 : 0;
     // f32: d + 1 fma-chain roundings, x4 margin.  split-f16: 3 K products per output summed in
     // f32 (<= 3K roundings), operand splitting 3 * 2^-22 = 12 * 2^-24, |c|^2 in f32 (d), x2.
@@ -1173,7 +1217,8 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
     const char* smp = getenv("MEPOL_KNN_SAMPLE");
     int S = smp ? atoi(smp) : 0;
     const int64_t nct = (nc + 31) / 32;
-    if (S < 2 || P->mode != 1 || nct / S < 8 || (int64_t)32 * (nct / S) < 4 * kp1) S = 0;
+    if (S < 2 || P->mode != 1 || P->KS16 > 3 || nct / S < 8 || (int64_t)32 * (nct / S) < 4 * kp1)
+      S = 0;
     P->sample = S;
     P->tau_list = 64;
     for (int v : kListChoices)
@@ -1327,6 +1372,25 @@ static int refine_rank_merge() {
   return v;
 }
 
+// KS16 = 4 (d + 1 in 49..64): double-buffered select16 with lists of at most 32, no sampling
+// pass (make_plan)
+static void launch_select16_ks4(const Plan& P, const _Float16* ap, const float* query,
+                                const unsigned* scal, float* tau, float* lv, int* li,
+                                hipStream_t st) {
+  const unsigned gx = (unsigned)((P.nqt + 3) / 4);
+#define MEPOL_SEL16W(L)                                                                          \
+  hipLaunchKernelGGL((select16_kernel<4, L, false>), dim3(gx, (unsigned)P.split), dim3(256), 0, \
+                     st, ap, query, P.nq, P.d, P.nct, P.split, P.tiles_per_split, 1, P.kp1, P.keep, \
+                     scal, tau, nullptr, lv, li)
+  switch (P.LIST16) {
+    case 8: MEPOL_SEL16W(8); break;
+    case 16: MEPOL_SEL16W(16); break;
+    case 24: MEPOL_SEL16W(24); break;
+    default: MEPOL_SEL16W(32); break;
+  }
+#undef MEPOL_SEL16W
+}
+
 template <int LIST>
 static void launch_refine_list(const Plan& P, const float* cand, const float* query,
                                const float* lv, const int* li, const unsigned* cmax,
@@ -1461,10 +1525,11 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
         MEPOL_CHECK_LAUNCH();
         continue;
       }
-      switch (P.KS16) {  // mode 1 only for KS16 <= 3 (make_plan)
+      switch (P.KS16) {  // mode 1 only for KS16 <= 3, or 4 with lists <= 32 (make_plan)
         case 1: launch_select16_ks<1>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
         case 2: launch_select16_ks<2>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
-        default: launch_select16_ks<3>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
+        case 3: launch_select16_ks<3>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
+        default: launch_select16_ks4(P, ap16, query, cmax, tau, lv, li, st); break;
       }
       MEPOL_CHECK_LAUNCH();
     }
