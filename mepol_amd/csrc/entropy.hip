@@ -107,8 +107,21 @@ __global__ __launch_bounds__(256) void entropy_fwd_kernel(
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   double th = 0.0, tk = 0.0;
   if (i < N) {
+    // 8 neighbours at a time: their ids, then their weights, all in flight before the first
+    // add (the per-neighbour loop serialised two dependent loads per neighbour); same order
     double Wi = 0.0;
-    for (int c = 0; c < k; ++c) Wi += w[idxT[(int64_t)c * N + i]];
+    constexpr int kCh = 8;
+    for (int c0 = 0; c0 < k; c0 += kCh) {
+      int id[kCh];
+#pragma unroll
+      for (int u = 0; u < kCh; ++u) id[u] = idxT[(int64_t)min(c0 + u, k - 1) * N + i];
+      double wv[kCh];
+#pragma unroll
+      for (int u = 0; u < kCh; ++u) wv[u] = w[id[u]];
+#pragma unroll
+      for (int u = 0; u < kCh; ++u)
+        if (c0 + u < k) Wi += wv[u];
+    }
     const double V = pow(D[i * kp1 + k], ns) * pi_ns2_over_G;
     const double r = Wi / (V + eps);
     const double lr = log(r + eps);
@@ -173,7 +186,7 @@ __global__ __launch_bounds__(256) void entropy_finalize_kernel(const double* __r
 // per lane group (one lane per particle with a serial loop over ~k ids was latency-bound at
 // 85 us for C3).  Fixed order: lane sums over a stride of 16, then an xor tree.
 constexpr int kGammaLanes = 16;
-constexpr int64_t kGammaMaxBlocks = 1024;
+constexpr int64_t kGammaMaxBlocks = 2048;  // 8 blocks (32 waves) per CU: full occupancy
 __global__ __launch_bounds__(256) void gamma_kernel(const double* __restrict__ g,
                                                     const double* __restrict__ w,
                                                     const int32_t* __restrict__ off,

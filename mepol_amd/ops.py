@@ -203,8 +203,8 @@ def entropy_gamma(g, w_own, csr_off, csr_rows):
     n_own = w_own.numel()
     dev = w_own.device
     gamma = torch.empty(n_own, dtype=torch.float64, device=dev)
-    # one partial per 256-thread block (16 lanes per particle), at most 1024 blocks
-    nparts = min((n_own * 16 + 255) // 256, 1024)
+    # one partial per 256-thread block (16 lanes per particle), at most 2048 blocks
+    nparts = min((n_own * 16 + 255) // 256, 2048)
     partials = torch.empty(max(nparts, 1), dtype=torch.float64, device=dev)
     call("mepol_entropy_gamma", ptr(g), ptr(w_own), ptr(csr_off), ptr(csr_rows), n_own,
          ptr(gamma), ptr(partials), _stream())
