@@ -864,6 +864,7 @@ __global__ __launch_bounds__(256) void refine_kernel(
     int64_t* __restrict__ I64, int32_t* __restrict__ I32, int* __restrict__ flag_count,
     int* __restrict__ flag_list, int rank_merge) {
   __shared__ int sel[4][64];
+  __shared__ float selv[4][64];  // rank merge: approximate value of sel[r]
   constexpr int kRM = MAXP <= 4 ? MAXP : 1;  // rank merge for M <= 256 entries
   __shared__ float2 sent[4][64 * kRM];        // rank merge: the query's entries (value, index bits)
   if (MAXP > 4) rank_merge = 0;
@@ -942,13 +943,13 @@ __global__ __launch_bounds__(256) void refine_kernel(
     for (int p = 0; p < MAXP; ++p) {
       if (ei[p] != INT_MAX && rk[p] < LIST) {
         sel[w][rk[p]] = ei[p];
-        if (rk[p] == LIST - 1) sent[w][0].x = ev[p];  // read back below as `last`
+        selv[w][rk[p]] = ev[p];
       }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     const int s_last = sel[w][LIST - 1];
-    last = (s_last >= 0) ? sent[w][0].x : INFINITY;
+    last = (s_last >= 0) ? selv[w][LIST - 1] : INFINITY;
   }
 #pragma nounroll
   for (int r = 0; r < (rank_merge ? 0 : LIST); ++r) {
@@ -981,11 +982,36 @@ __global__ __launch_bounds__(256) void refine_kernel(
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
-  // Exact f64 distances for the selected candidates, one per lane.
+  // |q|^2 and the selection's error bound E (certification below; any summation order)
   const float* xq = query + q * d;
+  double qn2 = 0.0;
+  for (int f = l; f < d; f += 64) qn2 += (double)xq[f] * (double)xq[f];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) qn2 += __shfl_xor(qn2, m, kWave);
+  const double cmax = (double)__uint_as_float(*cmax_bits);
+  // e_terms * 2^-24 * (C^2 + 2 C |q|) bounds the selection's error (f32 path: 4 (d + 1);
+  // split-f16 path: 2 (3 K + 16 + d), see make_plan), C = max candidate norm.
+  const double E = (double)e_terms * 5.9604644775390625e-08 *
+                       (cmax * cmax + 2.0 * cmax * sqrt(qn2)) + 1e-300;
+  // Rank merge: only the candidates within the error band of the (k+1)-th approximate value
+  // need exact distances.  Ranks >= mcut all have approx > v_(k+1) + 2.5 E: their exact d^2
+  // exceeds every exact d^2 of the first k+1 (each within E of its approx), and the first
+  // excluded value joins the certification bound, as the LIST-th did.
+  int mcut = LIST;
+  if (rank_merge && sel[w][kp1 - 1] >= 0) {
+    const double cut = (double)selv[w][kp1 - 1] + 2.5 * E;
+    const bool out = l >= kp1 && l < LIST && sel[w][l] >= 0 && (double)selv[w][l] > cut;
+    const unsigned long long ob = __ballot(out);
+    if (ob) {
+      mcut = __builtin_ctzll(ob);  // ranks are sorted: the first excluded one
+      bnd = fminf(bnd, selv[w][mcut]);
+    }
+  }
+
+  // Exact f64 distances for the selected candidates, one per lane.
   double dd = INFINITY;
   int di = INT_MAX;
-  if (l < LIST) {
+  if (l < mcut) {
     const int c = sel[w][l];
     if (c >= 0) {
       dd = exact_d2(xq, cand + (int64_t)c * d, d);
@@ -1010,16 +1036,8 @@ __global__ __launch_bounds__(256) void refine_kernel(
       }
     }
   }
-  // Certification: every candidate outside `sel` has exact d^2 >= bnd + |q|^2 - E.
-  double qn2 = 0.0;  // |q|^2 for the certification bound (any summation order)
-  for (int f = l; f < d; f += 64) qn2 += (double)xq[f] * (double)xq[f];
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) qn2 += __shfl_xor(qn2, m, kWave);
-  const double cmax = (double)__uint_as_float(*cmax_bits);
-  // e_terms * 2^-24 * (C^2 + 2 C |q|) bounds the selection's error (f32 path: 4 (d + 1);
-  // split-f16 path: 2 (3 K + 16 + d), see make_plan), C = max candidate norm.
-  const double E = (double)e_terms * 5.9604644775390625e-08 *
-                       (cmax * cmax + 2.0 * cmax * sqrt(qn2)) + 1e-300;
+  // Certification: every candidate outside the exactly evaluated set has exact
+  // d^2 >= bnd + |q|^2 - E.
   const double ek = __shfl(dd, kp1 - 1, kWave);
   const int eki = __shfl(di, kp1 - 1, kWave);
   bool ok = (eki != INT_MAX) && !overflow;
