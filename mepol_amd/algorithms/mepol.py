@@ -297,6 +297,7 @@ def collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len
     real_traj_lengths = rtl32.to(int_type)
     batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T)
     P.register(I, batch)
+    batch.csr(k)  # queued now: the GPU builds it while the host sets up the off-policy loop
     return states, actions, real_traj_lengths, next_states, D, I
 
 
@@ -306,6 +307,7 @@ def make_particle_batch(states, actions, real_traj_lengths, next_states_f32, k):
     D, I, I32T = ops.knn(next_states_f32, k + 1)
     batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T)
     P.register(I, batch)
+    batch.csr(k)  # queued now: the GPU builds it while the host sets up the off-policy loop
     return states, actions, real_traj_lengths, next_states_f32.to(float_type), D, I
 
 
@@ -755,9 +757,11 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
         loop = fns.make_device_loop(optimizer, behavioral_policy, target_policy)
     elif deferred and fns is sys.modules[__name__]:
         batch = P.lookup(states, actions, real_traj_lengths, distances, indices)
+        # queued first (every path needs it): the forward runs while the host checks and sets
+        # up the device loop
+        logp_b = batch.behavioral_logp(behavioral_policy)
         if device_loop.supported(batch, behavioral_policy, target_policy, optimizer):
             loop = device_loop.get(target_policy, optimizer, batch, k, G, B, ns, eps)
-            logp_b = batch.behavioral_logp(behavioral_policy)
             loop.load(batch, logp_b)
             # At an epoch's start the target holds the behavioral parameters (mepol.py:409, 493):
             # its log-probabilities are then logp_b itself, not another forward pass.
