@@ -117,8 +117,7 @@ class DeviceIteration:
         self.logp = torch.empty(self.N, **f64)
         self.fused_fwd = (ops.policy_forward_ok(self.x.shape[1], W2.shape[0])
                           and os.environ.get("MEPOL_FUSED_FWD", "1") != "0")
-        self.dh1_first = os.environ.get("MEPOL_DH1_FIRST", "0") != "0"
-        self.fused_dh1 = (ops.dh1_layer1_ok(self.x.shape[1], W2.shape[0]) and not self.dh1_first
+        self.fused_dh1 = (ops.dh1_layer1_ok(self.x.shape[1], W2.shape[0])
                           and os.environ.get("MEPOL_FUSED_DH1", "1") != "0")
         self.neg_one = torch.full((), -1.0, **f64)
         # every body takes its optimizer step through _optim_step, which leaves theta_t in the
@@ -149,8 +148,6 @@ class DeviceIteration:
         self.graph = None
         self.fork = torch.cuda.Stream(device=dev)
         self.s_gemm = torch.cuda.Stream(device=dev)
-        self.s_head = torch.cuda.Stream(device=dev)
-        self.ranges = _row_chunks(self.N)
         self._batch_id = None
         self._init_state()
 
@@ -248,63 +245,39 @@ class DeviceIteration:
             h[1], h[2], h[3] = lr, g["alpha"], g["eps"]
 
     # -- the iteration --------------------------------------------------------------------------
-    def load(self, batch, logp_b):
-        """Copy one epoch's particles and cached per-epoch tensors into the static inputs."""
+    def load(self, batch, logp_b=None):
+        """Copy one epoch's particles and cached per-epoch tensors into the static inputs.
+        Without logp_b the caller must follow with start_from_behavioral()."""
         off, rows = batch.csr(self.k)
-        for dst, src in ((self.x, batch.states_flat), (self.act, batch.actions_flat),
-                         (self.D, batch.D), (self.idx32T, batch.idx32T),
-                         (self.offsets, batch.offsets), (self.logp_b, logp_b),
-                         (self.csr_off, off), (self.csr_rows, rows)):
+        pairs = [(self.x, batch.states_flat), (self.act, batch.actions_flat), (self.D, batch.D),
+                 (self.idx32T, batch.idx32T), (self.offsets, batch.offsets),
+                 (self.csr_off, off), (self.csr_rows, rows)]
+        if logp_b is not None:
+            pairs.append((self.logp_b, logp_b))
+        for dst, src in pairs:
             dst.copy_(src)
         self._batch_id = id(batch)
 
     @torch.no_grad()
     def forward(self):
-        """logp of the target at its current parameters into the static buffers.
-
-        Row chunks are software-pipelined over three streams: layer 1 of chunk c+1 (HBM-bound,
-        current stream) and the head of chunk c-1 (HBM-bound, s_head) run while the f64 GEMM of
-        chunk c (MFMA-bound, s_gemm) does."""
+        """logp of the target at its current parameters into the static buffers (h1, z2, mu
+        and logp: the next replay's backward reads the activations)."""
         W1, b1, W2, b2, Wm, bm, ls = self.named
-        if self.fused_fwd:  # layer 1 + z2 GEMM + head in one kernel per row chunk
-            for r0, r1 in self.ranges:
-                ops.policy_forward(self.x[r0:r1], W1, b1, W2, b2, Wm, bm, ls, self.act[r0:r1],
-                                   self.h1[r0:r1], self.z2[r0:r1], self.mu[r0:r1],
-                                   self.logp[r0:r1])
+        if self.fused_fwd:  # layer 1 + z2 GEMM + head in one kernel
+            ops.policy_forward(self.x, W1, b1, W2, b2, Wm, bm, ls, self.act, self.h1, self.z2,
+                               self.mu, self.logp)
             return
-        if len(self.ranges) == 1:
-            ops.layer_forward(self.x, W1, b1, out=self.h1)
-            torch.mm(self.h1, W2.t(), out=self.z2)
-            ops.head_forward(self.z2, Wm, bm, ls, self.act, bz=b2, mu_out=self.mu,
-                             logp_out=self.logp)
-            return
-        cur = torch.cuda.current_stream()
-        self.s_gemm.wait_stream(cur)
-        self.s_head.wait_stream(cur)
-        for r0, r1 in self.ranges:
-            ops.layer_forward(self.x[r0:r1], W1, b1, out=self.h1[r0:r1])
-            e_l = torch.cuda.Event()
-            e_l.record(cur)
-            self.s_gemm.wait_event(e_l)
-            with torch.cuda.stream(self.s_gemm):
-                torch.mm(self.h1[r0:r1], W2.t(), out=self.z2[r0:r1])
-                e_g = torch.cuda.Event()
-                e_g.record(self.s_gemm)
-            self.s_head.wait_event(e_g)
-            with torch.cuda.stream(self.s_head):
-                ops.head_forward(self.z2[r0:r1], Wm, bm, ls, self.act[r0:r1], bz=b2,
-                                 mu_out=self.mu[r0:r1], logp_out=self.logp[r0:r1])
-        cur.wait_stream(self.s_gemm)
-        cur.wait_stream(self.s_head)
-
+        ops.layer_forward(self.x, W1, b1, out=self.h1)
+        torch.mm(self.h1, W2.t(), out=self.z2)
+        ops.head_forward(self.z2, Wm, bm, ls, self.act, bz=b2, mu_out=self.mu,
+                         logp_out=self.logp)
 
     def _backward(self, grad):
         """(dW1, db1, dW2, db2, dWm, dbm, dls) from dH/dlogp: the _TwoLayerLogp backward.
 
-        One chunk: head backward, then dW2 (split-K GEMM, forked stream) concurrent with
-        dh1 -> layer-1 backward.  Several chunks: the head backward of chunk c+1 (HBM-bound)
-        also overlaps the GEMMs of chunk c; per-chunk weight gradients are summed in chunk
-        order (fixed, so the result is reproducible)."""
+        Head backward, then dW2 (split-K GEMM, forked stream) concurrent with the fused
+        dh1 -> layer-1 backward (measured: faster than dh1 first with dW2 overlapping the
+        layer-1 backward, and than splitting dW2 across both phases)."""
         W1, b1, W2, b2, Wm, bm, ls = self.named
         cur = torch.cuda.current_stream()
         # W2^T for the fused dh1 kernel, on this stream: on a forked one the small copy kernel
@@ -312,53 +285,25 @@ class DeviceIteration:
         W2t = W2.t().contiguous() if self.fused_dh1 else None
         self.fork.wait_stream(cur)
         self.s_gemm.wait_stream(cur)
-        parts, keep = [], []
-        for r0, r1 in self.ranges:
-            sl = slice(r0, r1)
-            dz2, dWm, dbm, dls, db2 = ops.head_backward(grad[sl], self.z2[sl], Wm, ls,
-                                                        self.act[sl], self.mu[sl], bz=b2,
-                                                        need_dz=True, ws=self.ws_head)
-            e_h = torch.cuda.Event()
-            e_h.record(cur)
-            if self.dh1_first:
-                # dh1 alone (MFMA-bound, whole GPU), then dW2 (MFMA-bound) on the fork
-                # concurrent with the HBM-bound layer-1 backward, which therefore leaves the
-                # critical path (dh1 -> layer-1 backward was its tail).
-                self.s_gemm.wait_event(e_h)
-                with torch.cuda.stream(self.s_gemm):
-                    dh1 = torch.mm(dz2, W2)
-                    e_d = torch.cuda.Event()
-                    e_d.record(self.s_gemm)
-                    dW1, db1 = ops.layer_backward(dh1, self.h1[sl], self.x[sl],
-                                                  ws=self.ws_layer)
-                self.fork.wait_event(e_d)
-                with torch.cuda.stream(self.fork):
-                    dW2 = _weight_grad(dz2, self.h1[sl])
+        dz2, dWm, dbm, dls, db2 = ops.head_backward(grad, self.z2, Wm, ls, self.act, self.mu,
+                                                    bz=b2, need_dz=True, ws=self.ws_head)
+        e_h = torch.cuda.Event()
+        e_h.record(cur)
+        self.fork.wait_event(e_h)
+        with torch.cuda.stream(self.fork):
+            dW2 = _weight_grad(dz2, self.h1)
+        self.s_gemm.wait_event(e_h)
+        with torch.cuda.stream(self.s_gemm):
+            if self.fused_dh1:  # dh1 stays on chip (csrc/gemm.hip)
+                dh1 = None
+                dW1, db1 = ops.dh1_layer1_backward(dz2, W2t, self.h1, self.x, ws=self.ws_dh1)
             else:
-                # dW2 (split-K GEMM) on a forked stream, concurrent with dh1 -> layer-1
-                # backward (measured: faster than dh1 first with dW2 overlapping the layer-1
-                # backward, and than splitting dW2 across both phases).
-                self.fork.wait_event(e_h)
-                with torch.cuda.stream(self.fork):
-                    dW2 = _weight_grad(dz2, self.h1[sl])
-                self.s_gemm.wait_event(e_h)
-                with torch.cuda.stream(self.s_gemm):
-                    if self.fused_dh1:  # dh1 stays on chip (csrc/gemm.hip)
-                        dh1 = None
-                        dW1, db1 = ops.dh1_layer1_backward(dz2, W2t, self.h1[sl],
-                                                           self.x[sl], ws=self.ws_dh1)
-                    else:
-                        dh1 = torch.mm(dz2, W2)
-                        dW1, db1 = ops.layer_backward(dh1, self.h1[sl], self.x[sl],
-                                                      ws=self.ws_layer)
-            keep += [dz2, dh1]
-            parts.append((dW1, db1, dW2, db2, dWm, dbm, dls))
+                dh1 = torch.mm(dz2, W2)
+                dW1, db1 = ops.layer_backward(dh1, self.h1, self.x, ws=self.ws_layer)
         cur.wait_stream(self.fork)
         cur.wait_stream(self.s_gemm)
-        del keep
-        if len(parts) == 1:
-            return parts[0]
-        return tuple(torch.stack([p[i] for p in parts]).sum(0) for i in range(7))
+        del dz2, dh1
+        return dW1, db1, dW2, db2, dWm, dbm, dls
 
     @torch.no_grad()
     def _body(self):
@@ -418,15 +363,28 @@ class DeviceIteration:
         self.g_cur.copy_(g)
         self.out_cur.copy_(out)
 
-    def refresh(self, logp=None):
-        """Recompute the iteration's inputs that depend on theta (logp, w, dH/dW).  logp: the
-        target's log-probabilities when the caller already has them (the epoch's first step,
-        where the target holds the behavioral parameters)."""
-        if logp is None:
-            self.forward()
-        else:
-            self.logp.copy_(logp.reshape(-1))
+    def refresh(self):
+        """Recompute the iteration's inputs that depend on theta: the forward (h1, z2, mu and
+        logp, which the next replay's backward reads) and w, dH/dW."""
+        self.forward()
         self._prime()
+
+    def start_from_behavioral(self):
+        """Epoch start with the target holding the behavioral parameters (mepol.py:409, 493):
+        one forward fills h1/z2/mu/logp for the first replay's backward and is also the epoch's
+        behavioral logp_b (the same parameters).  Returns logp_b [nt, T]."""
+        self.forward()
+        self.logp_b.view(-1).copy_(self.logp)
+        self._prime()
+        return self.logp_b
+
+    def logp_of_last_step(self):
+        """logp at the parameters of the last step() result's theta_t+1, i.e. the final
+        accepted parameters.  Valid only when no replay is in flight and that step was the
+        last one launched (no speculative replay has overwritten the forward buffers)."""
+        if self._inflight or (self._last + 1) % len(self._bufs) != self._next:
+            raise RuntimeError("the forward buffers do not hold the last step's parameters")
+        return self.logp
 
     def _warmup(self):
         """One eager pass on a side stream (allocator pools, library handles, kernel code)."""
@@ -501,16 +459,6 @@ class DeviceIteration:
             torch._foreach_copy_(self.params, self._bufs[par]["shadow"])
             torch._foreach_add_([self.opt.state[p]["step"] for p in self.params], -1.0)
             self._next = par
-
-
-def _row_chunks(n):
-    """Row ranges of the pipelined forward/backward: MEPOL_ITER_CHUNKS (default 1) chunks of
-    at least 32768 rows (64-row aligned), one chunk for smaller batches."""
-    want = int(os.environ.get("MEPOL_ITER_CHUNKS", "1"))
-    c = max(1, min(want, n // 32768))
-    step = -(-n // c)
-    step = -(-step // 64) * 64
-    return [(r, min(n, r + step)) for r in range(0, n, step)]
 
 
 _CACHE = weakref.WeakKeyDictionary()  # target policy -> DeviceIteration

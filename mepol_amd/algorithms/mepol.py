@@ -757,15 +757,17 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
         loop = fns.make_device_loop(optimizer, behavioral_policy, target_policy)
     elif deferred and fns is sys.modules[__name__]:
         batch = P.lookup(states, actions, real_traj_lengths, distances, indices)
-        # queued first (every path needs it): the forward runs while the host checks and sets
-        # up the device loop
-        logp_b = batch.behavioral_logp(behavioral_policy)
         if device_loop.supported(batch, behavioral_policy, target_policy, optimizer):
             loop = device_loop.get(target_policy, optimizer, batch, k, G, B, ns, eps)
-            loop.load(batch, logp_b)
-            # At an epoch's start the target holds the behavioral parameters (mepol.py:409, 493):
-            # its log-probabilities are then logp_b itself, not another forward pass.
-            loop.refresh(logp=logp_b if _same_params(target_policy, behavioral_policy) else None)
+            if _same_params(target_policy, behavioral_policy):
+                # At an epoch's start the target holds the behavioral parameters (mepol.py:409,
+                # 493): one forward into the loop's buffers serves as logp_b and as the first
+                # replay's activations.
+                loop.load(batch)
+                batch.seed_behavioral_logp(behavioral_policy, loop.start_from_behavioral())
+            else:
+                loop.load(batch, batch.behavioral_logp(behavioral_policy))
+                loop.refresh()
     # device loop: the parameters before each replay's step are kept on the device (the last
     # accepted ones), so last_valid is only written when a step is rejected and at the end
     shadow = loop is not None and getattr(loop, "tracks_shadow", False)
@@ -840,7 +842,7 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
             if batch is not None:
                 # the last replay's forward ran at exactly these parameters: its logp serves
                 # the final entropy's forward of last_valid (mepol.py:466-468)
-                batch.seed_behavioral_logp(last_valid_target_policy, loop.logp)
+                batch.seed_behavioral_logp(last_valid_target_policy, loop.logp_of_last_step())
     with torch.no_grad():
         entropy = fns.compute_entropy(last_valid_target_policy, last_valid_target_policy, states,
                                       actions, num_traj, real_traj_lengths, distances, indices, k,

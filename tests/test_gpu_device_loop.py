@@ -16,8 +16,10 @@ SMALL = dict(NT=NT, T=T, NF=NF, A=A, K=K, HID=HID)
 C3 = dict(NT=40, T=500, NF=29, A=8, K=30, HID=[400, 300])
 C4 = dict(NT=40, T=500, NF=47, A=17, K=30, HID=[400, 300])
 C5 = dict(NT=400, T=50, NF=63, A=20, K=50, HID=[400, 300])
-# large enough for the 4-chunk pipelined forward/backward (algorithms/device_loop._row_chunks)
-BIG = dict(NT=256, T=512, NF=29, A=8, K=10, HID=[64, 48])
+# the full BASELINE batches the bench runs (C3: 400 x 500 = 200k particles; C5: 10000 x 50 =
+# 500k particles)
+C3_FULL = dict(NT=400, T=500, NF=29, A=8, K=30, HID=[400, 300])
+C5_FULL = dict(NT=10000, T=50, NF=63, A=20, K=50, HID=[400, 300])
 
 
 def _setup(opt_name, lr, seed=5, cfg=None):
@@ -94,11 +96,8 @@ def _assert_same_run(g, e):
     ("adam", 5e-2, 1e-3, SMALL),     # early rejection -> backtracking with halved lr
     ("rmsprop", 1e-4, 10.0, SMALL),
     ("adam", 1e-4, 10.0, C4),        # wide action head (a = 17)
-    ("adam", 1e-3, 10.0, BIG),       # 4 row chunks pipelined over three streams
 ])
 def test_graph_loop_matches_eager(cuda, monkeypatch, opt_name, lr, kl_threshold, cfg):
-    if cfg is BIG:  # the row-chunk pipeline is off by default (measured slower at C3)
-        monkeypatch.setenv("MEPOL_ITER_CHUNKS", "4")
     g = _run(monkeypatch, True, opt_name, lr, kl_threshold, cfg=cfg)
     e = _run(monkeypatch, False, opt_name, lr, kl_threshold, cfg=cfg)
     _assert_same_run(g, e)
@@ -125,20 +124,16 @@ def test_graph_loop_mid_loop_rejection(cuda, monkeypatch, backtracking, speculat
     _assert_same_run(g, e)
 
 
-@pytest.mark.parametrize("cfg,lr", [(SMALL, 1e-3), (C3, 1e-4), (C4, 1e-4), (C5, 1e-4)],
-                         ids=["small", "C3-shape", "C4-shape", "C5-shape"])
-def test_graph_loop_matches_oracle(cuda, monkeypatch, cfg, lr):
-    """Three accepted Adam steps against the oracle's torch-CPU policy_update/compute_kl, at the
-    BASELINE policy shapes (29/47/63 -> [400, 300] -> 8/17/20, k = 30/30/50; N = 20000)."""
+def _oracle_steps(g, cfg, lr, steps):
+    """Replay `steps` accepted Adam steps of the oracle's torch-CPU policy_update/compute_kl
+    (oracle/mepol_oracle.py, mepol.py:268-281, 157-174) from _setup's initial weights on the
+    same particles and the GPU's D/I; compare H, KL per step and the final parameters."""
     import oracle.mepol_oracle as O
-
-    NT, T, NF, A, K, HID = cfg["NT"], cfg["T"], cfg["NF"], cfg["A"], cfg["K"], cfg["HID"]
-    g = _run(monkeypatch, True, "adam", lr, 1e9, max_off_iters=3, cfg=cfg)
-    assert g["used"] and g["n"] == 3
-    states, actions = g["raw"]
-    torch.manual_seed(5)
     from mepol_amd.policy import GaussianPolicy
 
+    NT, T, NF, A, K, HID = cfg["NT"], cfg["T"], cfg["NF"], cfg["A"], cfg["K"], cfg["HID"]
+    states, actions = g["raw"]
+    torch.manual_seed(5)
     sd = GaussianPolicy(HID, NF, A).state_dict()  # the initial weights _setup drew
     beh = O.TorchPolicy(HID, NF, A)
     beh.load_state_dict(sd)
@@ -150,13 +145,33 @@ def test_graph_loop_matches_oracle(cuda, monkeypatch, cfg, lr):
     D, I = g["D"].cpu(), g["I"].cpu()
     G = float(scipy.special.gamma(NF / 2 + 1))
     B = float(np.log(K) - scipy.special.digamma(K))
-    for it in range(3):
+    for it in range(steps):
         loss, _ = O.torch_policy_update(opt, beh, tgt, S, Ac, NT, lengths, D, I, K, G, B, NF, 0.0)
         kl, _ = O.torch_kl(beh, tgt, S, Ac, NT, lengths, I, K, 0.0)
         np.testing.assert_allclose(g["trace"][it][1], -float(loss.detach()), rtol=1e-9)
-        np.testing.assert_allclose(g["trace"][it][2], float(kl), rtol=1e-7, atol=1e-12)
+        np.testing.assert_allclose(g["trace"][it][2], float(kl), rtol=1e-9, atol=1e-13)
     p = torch.cat([q.detach().reshape(-1) for q in tgt.parameters()]).numpy()
     np.testing.assert_allclose(g["params"], p, rtol=1e-7, atol=1e-10)
+
+
+@pytest.mark.parametrize("cfg,lr", [(SMALL, 1e-3), (C3, 1e-4), (C4, 1e-4), (C5, 1e-4)],
+                         ids=["small", "C3-shape", "C4-shape", "C5-shape"])
+def test_graph_loop_matches_oracle(cuda, monkeypatch, cfg, lr):
+    """Three accepted Adam steps against the oracle's torch-CPU policy_update/compute_kl, at the
+    BASELINE policy shapes (29/47/63 -> [400, 300] -> 8/17/20, k = 30/30/50; N = 20000)."""
+    g = _run(monkeypatch, True, "adam", lr, 1e9, max_off_iters=3, cfg=cfg)
+    assert g["used"] and g["n"] == 3
+    _oracle_steps(g, cfg, lr, 3)
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("cfg,steps", [(C3_FULL, 2), (C5_FULL, 1)], ids=["C3", "C5"])
+def test_graph_loop_matches_oracle_full_size(cuda, monkeypatch, cfg, steps):
+    """the graph-replayed iteration at the benchmarked sizes (C3 N = 200k,
+    d = 29, k = 30; C5 N = 500k, d = 63, k = 50) against the oracle's torch-CPU step."""
+    g = _run(monkeypatch, True, "adam", 1e-4, 1e9, max_off_iters=steps, cfg=cfg)
+    assert g["used"] and g["n"] == steps
+    _oracle_steps(g, cfg, 1e-4, steps)
 
 
 def _two_epochs(monkeypatch, graph):
@@ -195,13 +210,46 @@ def test_graph_scratch_survives_eager_growth(cuda, monkeypatch):
     np.testing.assert_allclose(g_params, e_params, rtol=1e-8, atol=1e-11)
 
 
-def test_row_chunks_cover_the_batch():
-    from mepol_amd.algorithms.device_loop import _row_chunks
+def _fresh_batch_epochs(monkeypatch, graph, thr):
+    """epoch 1 ends on a rejected step (no backtracking), epoch 2 runs on a
+    different batch of the same shape: the cached graph must take its activations from the new
+    batch at the new behavioral parameters, not from epoch 1's last (rejected) replay."""
+    monkeypatch.setenv("MEPOL_DEVICE_LOOP", "1" if graph else "0")
+    M, _, beh, tgt, last, opt, b1 = _setup("adam", 1e-3, seed=5)
+    b2 = _setup("adam", 1e-3, seed=6)[-1]
+    G = float(scipy.special.gamma(NF / 2 + 1))
+    Bc = float(np.log(K) - scipy.special.digamma(K))
+    out = []
+    for (st, ac, rl, _, D, I), t in ((b1, thr), (b2, 1e9)):
+        trace = []
+        res = M.off_policy_optimization(
+            opt, beh, tgt, last, st, ac, NT, rl, D, I, K, G, Bc, NF, 0.0, t, 6, False, 2, 4,
+            1e-3, on_accept=lambda n, e, kl, l: trace.append((n, float(e), float(kl))))
+        out.append((float(res[0]), res[1], trace))
+        beh.load_state_dict(last.state_dict())
+        tgt.load_state_dict(last.state_dict())
+    state = opt.state_dict()["state"]
+    moments = np.concatenate([state[i][key].detach().reshape(-1).cpu().numpy()
+                              for i in sorted(state) for key in sorted(state[i])
+                              if key != "step"])
+    params = torch.cat([p.detach().reshape(-1) for p in last.parameters()]).cpu().numpy()
+    return out, params, moments
 
-    for n in (1, 20000, 65535, 131072, 200000, 500000):
-        r = _row_chunks(n)
-        assert r[0][0] == 0 and r[-1][1] == n
-        assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
-        assert all(r1 > r0 for r0, r1 in r)
-        assert all(r0 % 64 == 0 for r0, _ in r)
-    assert len(_row_chunks(20000)) == 1
+
+def test_graph_loop_fresh_batch_after_rejection(cuda, monkeypatch):
+    probe = _run(monkeypatch, False, "adam", 1e-3, 1e9, max_off_iters=6)
+    kls = [t[2] for t in probe["trace"]]
+    cut = [i for i in range(1, len(kls)) if kls[i] > max(kls[:i])]
+    assert cut, kls
+    i = cut[-1]
+    thr = 0.5 * (max(kls[:i]) + kls[i])
+    g_out, g_params, g_mom = _fresh_batch_epochs(monkeypatch, True, thr)
+    e_out, e_params, e_mom = _fresh_batch_epochs(monkeypatch, False, thr)
+    assert g_out[0][1] == e_out[0][1] == i  # epoch 1: i accepted steps, then the rejection
+    for (gH, gn, gt), (eH, en, et) in zip(g_out, e_out):
+        assert gn == en and len(gt) == len(et)
+        np.testing.assert_allclose(gH, eH, rtol=1e-9)
+        for a, b in zip(gt, et):
+            np.testing.assert_allclose(a[1:], b[1:], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(g_params, e_params, rtol=1e-8, atol=1e-11)
+    np.testing.assert_allclose(g_mom, e_mom, rtol=1e-8, atol=1e-14)

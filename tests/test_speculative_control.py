@@ -45,11 +45,20 @@ class _FakeLoop:
         self.last = None
         self.logp = torch.zeros(1, dtype=torch.float64)
 
-    def load(self, batch, logp_b):
+    def load(self, batch, logp_b=None):
         pass
 
-    def refresh(self, logp=None):
+    def refresh(self):
         pass
+
+    def start_from_behavioral(self):
+        return self.logp
+
+    def logp_of_last_step(self):
+        # the device loop's contract: nothing in flight and the returned step launched last
+        assert not self.inflight and self.last["i"] == self.s["next"] - 1
+        self.s["final_logp_reads"] += 1
+        return self.logp
 
     def _launch(self):
         s = self.s
@@ -98,7 +107,8 @@ def _strip_time(csv1):
 def test_speculative_loop_matches_reference_control(name, tmp_path, monkeypatch):
     z = load_golden(f"control_{name}")
     sc = json.loads(str(z["scenario"]))
-    state = {"sc": sc, "next": 0, "trace": [], "launched": 0, "speculative": 0, "cancelled": 0}
+    state = {"sc": sc, "next": 0, "trace": [], "launched": 0, "speculative": 0, "cancelled": 0,
+             "final_logp_reads": 0}
 
     def fake_collect(env, pol, num_traj, traj_len, state_filter, k, num_workers):
         zz = torch.zeros((num_traj, traj_len + 1, 2), dtype=torch.float64)
