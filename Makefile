@@ -7,7 +7,13 @@ SRC     := $(wildcard mepol_amd/csrc/*.hip)
 OBJ     := $(patsubst mepol_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB     := mepol_amd/libmepol_amd.so
 
-all: $(LIB)
+ORACLE_NATIVE := oracle/native/librollout_kordered.so
+
+all: $(LIB) $(ORACLE_NATIVE)
+
+# the parity oracle's k-ordered rollout (test infrastructure; never linked into the product)
+$(ORACLE_NATIVE): oracle/native/rollout_kordered.c
+	gcc -O2 -ffp-contract=off -fPIC -shared $< -o $@ -lm
 
 build/%.o: mepol_amd/csrc/%.hip mepol_amd/csrc/common.hpp include/mepol_amd.h
 	@mkdir -p build
@@ -24,6 +30,6 @@ resource-usage:
 	@for f in $(SRC); do $(HIPCC) $(FLAGS) -Iinclude -c $$f -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|Scratch|Occupancy"; done
 
 clean:
-	rm -rf build $(LIB)
+	rm -rf build $(LIB) $(ORACLE_NATIVE)
 
 .PHONY: all clean resource-usage

@@ -44,10 +44,19 @@ WORKLOADS = {
                name="C4 Humanoid-shaped MEPOL epoch (k-NN + off-policy loop + final H)"),
     "C5": dict(COMMON, num_traj=10000, traj_len=50, nf=63, a=20, hidden=[400, 300], k=50, d=63,
                name="C5 HandReach-shaped MEPOL epoch (k-NN + off-policy loop + final H)"),
-    # one rank's particle share of C3 on 8 GPUs, run alone (no collectives, k-NN over its own
-    # 25k particles only): the compute floor of a rank in the 8-GPU strong-scaling run
-    "C3R8": dict(COMMON, num_traj=50, traj_len=500, nf=29, a=8, hidden=[400, 300], k=30, d=29,
-                 name="C3 per-rank share at 8 GPUs (25k particles, single GPU, no collectives)"),
+    # Rank 0 of the 8-GPU strong-scaling run, emulated on one GPU (_EmulatedDist): its 1/8 of
+    # the particles through the sharded code path (ShardedEpoch + ShardedIteration), the k-NN of
+    # its queries against ALL N candidates, every collective replaced by local copies of the
+    # same size (no peers, no xGMI): the per-rank compute of C3/C4/C5 at 8 GPUs.
+    "C3R8": dict(COMMON, num_traj=400, traj_len=500, nf=29, a=8, hidden=[400, 300], k=30, d=29,
+                 emulate_world=8,
+                 name="C3 rank-0 share at 8 GPUs (25k of 200k particles; k-NN vs all 200k)"),
+    "C4R8": dict(COMMON, num_traj=400, traj_len=500, nf=47, a=17, hidden=[400, 300], k=30, d=47,
+                 emulate_world=8,
+                 name="C4 rank-0 share at 8 GPUs (25k of 200k particles; k-NN vs all 200k)"),
+    "C5R8": dict(COMMON, num_traj=10000, traj_len=50, nf=63, a=20, hidden=[400, 300], k=50,
+                 d=63, emulate_world=8,
+                 name="C5 rank-0 share at 8 GPUs (62.5k of 500k particles; k-NN vs all 500k)"),
     "C2": dict(COMMON, num_traj=20, traj_len=1000, nf=2, a=2, hidden=[300, 300], k=4, d=2,
                log_std_init=-1.5, env="GridWorld",
                name="C2 GridWorld MEPOL epoch (GPU rollout + k-NN + off-policy loop + final H)"),
@@ -119,6 +128,43 @@ def synthetic_batch(cfg, seed, device, rank=0, world=1):
     actions = 0.5 * torch.randn((nt, T, a), generator=g, device=device, dtype=torch.float32)
     return (states[rank * per:(rank + 1) * per].contiguous(),
             actions[rank * per:(rank + 1) * per].contiguous())
+
+
+class _EmulatedDist:
+    """Rank 0 of a `world`-rank job on one GPU, without peers: the torch.distributed calls that
+    ShardedEpoch / ShardedIteration make, each replaced by local copies of the same size.
+    all_gather_into_tensor fills the peers' slots from `peers` (a list of world - 1 tensors)
+    when one of that shape and dtype is registered -- the other shards' next states, so the
+    k-NN runs against the full candidate set -- and with rank 0's own payload otherwise;
+    all_reduce keeps rank 0's values.  Per-rank compute of the multi-GPU run, not its result."""
+
+    class ReduceOp:
+        SUM, MIN, MAX = "sum", "min", "max"
+
+    def __init__(self, world):
+        self.world = world
+        self.peers = []
+
+    def get_world_size(self, group=None):
+        return self.world
+
+    def get_rank(self, group=None):
+        return 0
+
+    def get_backend(self, group=None):
+        return "nccl"  # the graph path captures these copies like RCCL collectives
+
+    def all_gather_into_tensor(self, out, inp, group=None):
+        o = out.view(self.world, -1)
+        flat = inp.reshape(-1)
+        o[0].copy_(flat)
+        pe = self.peers
+        src = pe if (pe and pe[0].shape == inp.shape and pe[0].dtype == inp.dtype) else None
+        for r in range(1, self.world):
+            o[r].copy_(src[r - 1].reshape(-1) if src is not None else flat)
+
+    def all_reduce(self, t, op=None, group=None):
+        return None
 
 
 def selftest(args):
@@ -194,7 +240,14 @@ def run(args):
     # MEPOL_BENCH_SHARDED=1 runs the multi-rank code path (ShardedEpoch + captured RCCL
     # collectives) at world size 1: a one-GPU rehearsal of what --gpus N runs per rank.
     sharded = world > 1 or os.environ.get("MEPOL_BENCH_SHARDED") == "1"
-    if sharded:
+    emul = None
+    if cfg.get("emulate_world"):
+        if world > 1:
+            raise SystemExit(f"bench: {args.workload} emulates one rank of "
+                             f"{cfg['emulate_world']} on one GPU; run it with --gpus 1")
+        emul = _EmulatedDist(cfg["emulate_world"])
+        sharded = True
+    if sharded and emul is None:
         import torch.distributed as dist
 
         _quiet_stdout()
@@ -218,8 +271,9 @@ def run(args):
 
     k, nf, a, d = cfg["k"], cfg["nf"], cfg["a"], cfg["d"]
     nt, T = cfg["num_traj"], cfg["traj_len"]
-    if nt % world:
-        raise SystemExit(f"bench: {nt} trajectories do not split over {world} ranks")
+    shards = emul.world if emul is not None else world   # ranks the particles are split over
+    if nt % shards:
+        raise SystemExit(f"bench: {nt} trajectories do not split over {shards} ranks")
     ns = d
     B = float(np.log(k) - scipy.special.digamma(k))
     G = float(scipy.special.gamma(ns / 2 + 1))
@@ -243,7 +297,12 @@ def run(args):
     opt = torch.optim.Adam(target.parameters(), lr=cfg["lr"])
     N = nt * T
 
-    batches = [] if rollout else [synthetic_batch(cfg, s, dev, rank, world) for s in range(3)]
+    batches = [] if rollout else [synthetic_batch(cfg, s, dev, rank, shards) for s in range(3)]
+    peers = []  # emulation: the other shards' next states of each batch (k-NN candidates)
+    if emul is not None:
+        for s_ in range(3):
+            peers.append([synthetic_batch(cfg, s_, dev, r, shards)[0][:, 1:].reshape(-1, nf)
+                          [:, :d].contiguous() for r in range(1, shards)])
     knn_events, roll_events, iters_done, entropies = [], [], [], []
 
     def one_epoch(i):
@@ -275,7 +334,9 @@ def run(args):
         else:
             from mepol_amd.parallel import ShardedEpoch
 
-            ep = ShardedEpoch(st, ac, rtl, nxt, k, dist)
+            if emul is not None:
+                emul.peers = peers[i % len(peers)]
+            ep = ShardedEpoch(st, ac, rtl, nxt, k, emul if emul is not None else dist)
             ep.build_knn()
             e2.record()
             res = ep.off_policy_optimization(
@@ -327,26 +388,16 @@ def run(args):
 
     it = (parallel._SHARDED_CACHE if sharded else device_loop._CACHE).get(target)
     iteration_path = "hip-graph replay" if it is not None and it.graph is not None else "eager"
-    nq = N // world
+    nq = N // shards
     F = 3.0 * d * nq * N                      # algorithmic flops
     knn_tflops = F / (knn_ms * 1e-3) / 1e12
-    # Which selection the library ran (include/mepol_amd.h; MEPOL_KNN_PRECISION=f32 forces f32):
-    # split-f16 issues 3 products x 2 x K flops per (query, candidate), K = 16*ceil((d+1)/16).
-    # (make_plan in csrc/knn.hip: split-f16 for KS16 <= 3 with lists <= 40 (32 at KS16 = 3),
-    # and KS16 = 4 with lists <= 32)
-    ks16 = (d + 1 + 15) // 16
-    keep = (k + 2) // 2 + 2
-    list16 = next((v for v in (8, 16, 24, 32, 40) if v >= keep + 4), 64)
-    f16_sel = (ks16 <= 3 and list16 <= (32 if ks16 == 3 else 40)) or (ks16 == 4 and list16 <= 32)
-    if os.environ.get("MEPOL_KNN_PRECISION", "") != "f32" and f16_sel:
-        K16 = 16 * ks16
-        knn_issued = 3 * 2 * K16 * float(nq) * N
-        knn_peak = PEAK_F16_TFLOPS
-        knn_desc = "split-f16 MFMA selection (3 products, f32 accumulate) + f64 exact refine (bit-exact output)"
-    else:
-        knn_issued = 2 * 2 * ((d + 2) // 2) * float(nq) * N
-        knn_peak = PEAK_FP32_TFLOPS
-        knn_desc = "fp32 MFMA selection + f64 exact refine (bit-exact output)"
+    # The selection (csrc/knn.hip): candidate-hi f16 MFMA, 2 products (q_hi, q_lo) x 2 x K flops
+    # per (query, candidate), K = 16*ceil((d+1)/16), f32 accumulate; then the f64 refine.
+    K16 = 16 * ((d + 1 + 15) // 16)
+    knn_issued = 2 * 2 * K16 * float(nq) * N
+    knn_peak = PEAK_F16_TFLOPS
+    knn_desc = ("f16 MFMA selection (candidate hi half x split query, f32 accumulate) + "
+                "certified f64 exact refine (bit-exact output)")
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"knn_pmc_{args.workload}.json")
     if args.workload == "C3" and not os.path.exists(pmc_path):
@@ -373,9 +424,12 @@ def run(args):
         "data": "synthetic" if not rollout else "GridWorld rollouts of a random-init policy",
         "config": {"workload": cfg["name"], "particles": N, "num_traj": nt, "traj_len": T,
                    "d": d, "k": k, "policy": f"{nf}->{cfg['hidden']}->{a} f64",
-                   "off_policy_iters": float(np.mean(iters_done)), "parallelism": f"dp{world}",
+                   "off_policy_iters": float(np.mean(iters_done)),
+                   "parallelism": (f"rank 0 of dp{shards} emulated on 1 GPU (collectives -> local "
+                                   f"copies of the same size)" if emul is not None
+                                   else f"dp{world}"),
                    "knn_precision": knn_desc, "off_policy_iteration": iteration_path},
-        "particles_per_s": round(N / epoch_s, 1),
+        "particles_per_s": round(N / shards / epoch_s, 1),
         "knn_ms": round(knn_ms, 3),
         "knn_ms_per_rank": [round(x, 3) for x in per_rank_knn],
         "roofline": {"bound": "mfma", "achieved": round(knn_tflops, 2), "peak": knn_peak,
@@ -399,7 +453,7 @@ def run(args):
         line["survey_reference_epoch_s"] = 9.10 if args.workload == "C2S" else None
     if rehearsal:
         line["config"]["rehearsal"] = f"{world} ranks on {torch.cuda.device_count()} GPU(s), gloo"
-    if not args.no_cpu_baseline and world == 1:
+    if not args.no_cpu_baseline and world == 1 and emul is None:
         line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample_queries, iters_done)
     _emit(line)
     if dist is not None:

@@ -11,7 +11,10 @@
  *    data_ptr()); nothing is allocated inside a call.  Scratch comes from a caller-owned
  *    workspace whose size the *_workspace_size query returns.
  *  - `stream` is a hipStream_t; every call only enqueues work on it (no host sync), so calls
- *    can be captured into a hipGraph.
+ *    can be captured into a hipGraph -- with ONE exception: mepol_knn synchronises `stream`
+ *    once per call to validate its input before the scan (sklearn raises on NaN / inf), so it
+ *    is never captured; the per-iteration entry points (entropy, IW, head, GEMMs, optimizer)
+ *    never synchronise.
  *  - Return value: 0 on success, a hipError_t value or one of the MEPOL_ERR_* codes otherwise;
  *    mepol_last_error_string() describes the last failure of the calling thread.
  *  - Stateless and re-entrant; ordering comes from the stream.
@@ -109,7 +112,8 @@ int mepol_entropy_reverse_scan(const double* gamma, const double* w, const doubl
                                double* grad_logp, void* stream);
 
 /* Whole rollout of collect_particles (mepol.py:70-111, one call for all T steps) for the
- * reference's 2-hidden-layer ReLU policy on a 2-feature env: one workgroup per trajectory.
+ * reference's 2-hidden-layer ReLU policy on a 2-feature env: one or ceil(h1/64) workgroups per
+ * trajectory (see mepol_rollout_mlp_workspace_size).
  * env_id 0 = MountainCar (init64 [n,2] f64), 1 = GridWorld (init32 [n,2] f32, a_dim = 2).
  * W1 [h0,2], b1 [h0], W2t = W2^T [h0,h1], b2 [h1], Wm [a_dim,h1], bm, log_std [a_dim];
  * noise [T,n,a_dim] f64 (a = mean + noise * exp(log_std), policy.py:59).  Writes states_rec
@@ -119,7 +123,14 @@ int mepol_rollout_mlp(int env_id, const double* W1, const double* b1, int h0, co
                       const double* b2, int h1, const double* Wm, const double* bm,
                       const double* log_std, int a_dim, const double* init64, const float* init32,
                       const double* noise, int64_t n, int64_t T, float* states_rec,
-                      float* actions_rec, double* visited, double* final_state, void* stream);
+                      float* actions_rec, double* visited, double* final_state, void* workspace,
+                      size_t workspace_bytes, void* stream);
+/* Scratch for mepol_rollout_mlp's multi-workgroup form (ceil(h1/64) workgroups per trajectory,
+ * each holding its 64 columns of W2^T in LDS; used when n * ceil(h1/64) fits the CUs and
+ * h0 <= 312).  Word 0 of the workspace is a device int32 error flag: 1 = the workgroups of a
+ * trajectory could not all run at once (results invalid; the caller raises).  A null or short
+ * workspace selects the one-workgroup-per-trajectory form (same results, bitwise). */
+int mepol_rollout_mlp_workspace_size(int64_t n, int h0, int h1, size_t* bytes);
 
 /* ---- policy MLP (GaussianPolicy, src/policy.py:16-51) for the large-batch passes -----------
  * Gaussian head: mean layer + log-probability with the last hidden layer's bias and ReLU folded
@@ -173,10 +184,6 @@ int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double*
 int mepol_gemm_nt(const double* A, int64_t n, int k, int64_t lda, const double* B, int m,
                   int64_t ldb, const double* bias, int relu, double* C, int64_t ldc, int variant,
                   void* stream);
-/* Tuning experiment: the same product on the VALU (v_fmac_f64 with DPP row broadcast). */
-int mepol_gemm_dpp(const double* A, int64_t n, int k, int64_t lda, const double* B, int m,
-                   int64_t ldb, const double* bias, int relu, double* C, int64_t ldc, int variant,
-                   void* stream);
 
 /* ---- environments -------------------------------------------------------------------------
  * Replace MountainCarContinuous.step (src/envs/mountain_car_wall.py:13-45) and

@@ -56,15 +56,14 @@ SIGNATURES = {
                                   _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_gemm_nt": [_c_vp, _c_i64, _c_int, _c_i64, _c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_vp,
                       _c_i64, _c_int, _c_vp],
-    "mepol_gemm_dpp": [_c_vp, _c_i64, _c_int, _c_i64, _c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_vp,
-                       _c_i64, _c_int, _c_vp],
     "mepol_step_mountaincar": [_c_vp, _c_vp, _c_i64, _c_i64, _c_vp],
     "mepol_step_gridworld": [_c_vp, _c_vp, _c_i64, _c_vp],
     "mepol_rollout_step": [_c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_i64,
                            _c_i64, _c_vp, _c_vp, _c_vp, _c_vp],
     "mepol_rollout_mlp": [_c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp, _c_vp,
                           _c_int, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp,
-                          _c_vp],
+                          _c_vp, _c_sz, _c_vp],
+    "mepol_rollout_mlp_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
     "mepol_memcpy_async": [_c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_optim_step": [_c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
     "mepol_optim_step_snapshot": [_c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,

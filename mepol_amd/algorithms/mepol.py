@@ -839,10 +839,12 @@ def off_policy_optimization(optimizer, behavioral_policy, target_policy, last_va
         loop.cancel()  # nothing is in flight here; kept as a guard
         if last_accepted:
             _copy_policy(last_valid_target_policy, target_policy)
-            if batch is not None:
-                # the last replay's forward ran at exactly these parameters: its logp serves
-                # the final entropy's forward of last_valid (mepol.py:466-468)
-                batch.seed_behavioral_logp(last_valid_target_policy, loop.logp_of_last_step())
+            # the last replay's forward ran at exactly these parameters: its logp serves the
+            # final entropy's forward of last_valid (mepol.py:466-468)
+            seed = batch.seed_behavioral_logp if batch is not None else getattr(
+                fns, "seed_behavioral_logp", None)
+            if seed is not None:
+                seed(last_valid_target_policy, loop.logp_of_last_step())
     with torch.no_grad():
         entropy = fns.compute_entropy(last_valid_target_policy, last_valid_target_policy, states,
                                       actions, num_traj, real_traj_lengths, distances, indices, k,

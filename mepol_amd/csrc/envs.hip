@@ -278,6 +278,170 @@ __global__ __launch_bounds__(kRollMaxH) void rollout_mlp_kernel(
     final_state[2 * i + 1] = sx[1];
   }
 }
+
+// ---- whole rollout, several workgroups per trajectory --------------------------------------
+// rollout_mlp_kernel puts a trajectory on ONE CU, which then streams most of W2^T from L2 every
+// step (11.7 us per step at C2's [300, 300]).  Here NP = ceil(h1 / 64) single-wave workgroups
+// share a trajectory: workgroup p owns hidden-2 columns [64 p, 64 p + 64) -- exactly wave p of
+// rollout_mlp_kernel -- and keeps their W2^T slice ([h0][64] f64, <= 156 KB) in LDS for all T
+// steps.  Per step every workgroup computes layer 1 (all h0 columns, redundantly), its 64
+// layer-2 columns (k-ordered fma chain) and its wave partial of the mean layer (the same
+// shuffle tree); the NP partials are exchanged through global memory (sc1 stores, a per-part
+// step flag behind s_waitcnt vmcnt(0), sc1 polls and loads: MI355X_MICROARCH.md's first
+// hand-off row) and every lane of every workgroup sums them in part order, adds the noise and
+// steps the env.  Same operations in the same order as rollout_mlp_kernel: bitwise identical
+// results.  Needs all n * NP workgroups resident at once (one per CU): the host launches it only
+// when n * NP <= the CU count; the flag polls are bounded (err = 1 instead of a hang).
+template <int ENV>
+__global__ __launch_bounds__(64) void rollout_mlp_mw_kernel(
+    const double* __restrict__ W1, const double* __restrict__ b1, int h0,
+    const double* __restrict__ W2t, const double* __restrict__ b2, int h1,
+    const double* __restrict__ Wm, const double* __restrict__ bm,
+    const double* __restrict__ log_std, int a_dim, const double* __restrict__ init64,
+    const float* __restrict__ init32, const double* __restrict__ noise, int64_t n, int64_t T,
+    float* __restrict__ states_rec, float* __restrict__ actions_rec,
+    double* __restrict__ visited, double* __restrict__ final_state, int np, int nw,
+    unsigned long long* __restrict__ mail, unsigned* __restrict__ flags, int* __restrict__ err) {
+  extern __shared__ double sW2[];  // [h0][64]: W2^T rows, this part's 64 columns
+  __shared__ double sh1[kRollMaxH];
+  const int64_t i = blockIdx.x / np;
+  const int p = (int)(blockIdx.x % np);
+  const int lane = threadIdx.x;
+  const int j = 64 * p + lane;
+  const bool c1 = j < h1;
+  for (int k = 0; k < h0; ++k) sW2[k * 64 + lane] = c1 ? W2t[(int64_t)k * h1 + j] : 0.0;
+  constexpr int kU = kRollMaxH / 64;  // layer-1 columns per lane
+  double w1a[kU], w1b[kU], bb1[kU];
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    const int c = lane + 64 * u;
+    const bool ok = c < h0;
+    w1a[u] = ok ? W1[2 * c] : 0.0;
+    w1b[u] = ok ? W1[2 * c + 1] : 0.0;
+    bb1[u] = ok ? b1[c] : 0.0;
+  }
+  const double bb2 = c1 ? b2[j] : 0.0;
+  double wm[kRollMaxA], sd[kRollMaxA], nz[kRollMaxA];
+#pragma unroll
+  for (int a = 0; a < kRollMaxA; ++a) {
+    wm[a] = (c1 && a < a_dim) ? Wm[a * h1 + j] : 0.0;
+    sd[a] = a < a_dim ? exp(log_std[a]) : 0.0;
+    nz[a] = a < a_dim ? noise[i * a_dim + a] : 0.0;
+  }
+  // env state, stepped identically by every lane of every part of the trajectory
+  double pp = 0.0, vv = 0.0, x0, x1;
+  float gx = 0.f, gy = 0.f;
+  if (ENV == 0) {
+    pp = init64[2 * i];
+    vv = init64[2 * i + 1];
+    x0 = pp;
+    x1 = vv;
+  } else {
+    gx = init32[2 * i];
+    gy = init32[2 * i + 1];
+    x0 = (double)gx;
+    x1 = (double)gy;
+  }
+  const bool rec = p == 0 && lane == 0;
+  if (rec) {
+    states_rec[(i * (T + 1)) * 2 + 0] = (float)x0;
+    states_rec[(i * (T + 1)) * 2 + 1] = (float)x1;
+  }
+  unsigned* myflags = flags + i * np;
+  __syncthreads();
+  for (int64_t t = 0; t < T; ++t) {
+    double nz_next[kRollMaxA];
+    if (t + 1 < T)
+      for (int a = 0; a < a_dim; ++a) nz_next[a] = noise[((t + 1) * n + i) * a_dim + a];
+    // layer 1 (nf = 2), every column
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int c = lane + 64 * u;
+      if (c < h0)
+        sh1[c] = fmax(__dadd_rn(__dadd_rn(__dmul_rn(x0, w1a[u]), __dmul_rn(x1, w1b[u])), bb1[u]),
+                      0.0);
+    }
+    __syncthreads();
+    // layer 2, this part's columns: h2_j = relu(sum_k W2[j][k] h1[k] + b2[j]), k in order
+    double acc = 0.0;
+    for (int k = 0; k < h0; ++k) acc = fma(sW2[k * 64 + lane], sh1[k], acc);
+    const double h2 = c1 ? fmax(acc + bb2, 0.0) : 0.0;
+    // mean layer: this part's wave partial (the shuffle tree of rollout_mlp_kernel), lane 0's
+    unsigned long long* slot = mail + ((i * 2 + (t & 1)) * np) * kRollMaxA;
+#pragma unroll
+    for (int a = 0; a < kRollMaxA; ++a) {
+      if (a < a_dim) {
+        double q = wm[a] * h2;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m, kWave);
+        if (lane == 0)
+          __hip_atomic_store(slot + p * kRollMaxA + a, __double_as_longlong(q), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0)
+      __hip_atomic_store(myflags + p, (unsigned)(t + 1), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    // wait for every part's partial of this step (lane q < np polls part q)
+    {
+      unsigned spins = 0;
+      bool bad = false;
+      while (true) {
+        const bool ok = lane >= np || __hip_atomic_load(myflags + lane, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) >=
+                                          (unsigned)(t + 1);
+        if (!__ballot(!ok)) break;
+        if (++spins > (1u << 24)) {
+          bad = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (bad) {
+        if (lane == 0) atomicExch(err, 1);
+        return;
+      }
+    }
+    double act[kRollMaxA];
+    for (int a = 0; a < a_dim; ++a) {
+      double mu = __longlong_as_double(
+          __hip_atomic_load(slot + a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      for (int q = 1; q < np; ++q)
+        mu += __longlong_as_double(__hip_atomic_load(slot + q * kRollMaxA + a, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT));
+      for (int q = np; q < nw; ++q) mu += 0.0;  // rollout_mlp_kernel's waves without columns
+      mu += bm[a];
+      // output = mean + randn * exp(log_std)   (policy.py:59)
+      act[a] = __dadd_rn(mu, __dmul_rn(nz[a], sd[a]));
+      if (rec) actions_rec[(i * T + t) * a_dim + a] = (float)act[a];
+    }
+    if (t + 1 < T)
+      for (int a = 0; a < a_dim; ++a) nz[a] = nz_next[a];
+    if (ENV == 0) {
+      MountainCar::step(pp, vv, act[0]);
+      x0 = pp;
+      x1 = vv;
+    } else {
+      GridWorld::step(gx, gy, act[0], act[1]);
+      x0 = (double)gx;
+      x1 = (double)gy;
+    }
+    if (rec) {
+      states_rec[(i * (T + 1) + t + 1) * 2 + 0] = (float)x0;
+      states_rec[(i * (T + 1) + t + 1) * 2 + 1] = (float)x1;
+      if (visited) {
+        visited[(i * T + t) * 2 + 0] = x0;
+        visited[(i * T + t) * 2 + 1] = x1;
+      }
+    }
+    __syncthreads();
+  }
+  if (rec && final_state) {
+    final_state[2 * i] = x0;
+    final_state[2 * i + 1] = x1;
+  }
+}
 }  // namespace envs
 }  // namespace mepol
 
@@ -329,12 +493,29 @@ extern "C" int mepol_rollout_step(int env_id, double* env_f64, float* env_f32, c
 // nf = 2 -> [h0, h1] -> a_dim with ReLU: W1 [h0,2], b1, W2t = W2^T [h0,h1], b2, Wm [a,h1], bm,
 // log_std [a]; noise [T,n,a_dim] f64.  Writes states_rec [n,T+1,2] f32, actions_rec [n,T,a] f32,
 // visited [n,T,2] f64 (nullable), final_state [n,2] f64 (nullable).
+// Multi-workgroup form: mail [n][2][np][kRollMaxA] (8-byte words), flags [n][np], err (word 0).
+static size_t rollout_mw_bytes(int64_t n, int h1) {
+  const int64_t np = (h1 + 63) / 64;
+  return 256 + align_up((size_t)n * 2 * np * kRollMaxA * 8, 256) + (size_t)n * np * 4;
+}
+static constexpr int kRollMwMaxH0 = 312;  // [h0][64] f64 slice + sh1 within 160 KB of LDS
+
+extern "C" int mepol_rollout_mlp_workspace_size(int64_t n, int h0, int h1, size_t* bytes) {
+  if (n < 0 || h0 <= 0 || h1 <= 0 || !bytes) {
+    set_error("mepol_rollout_mlp_workspace_size: bad arguments");
+    return kErrBadArg;
+  }
+  *bytes = rollout_mw_bytes(n, h1);
+  return 0;
+}
+
 extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1, int h0,
                                  const double* W2t, const double* b2, int h1, const double* Wm,
                                  const double* bm, const double* log_std, int a_dim,
                                  const double* init64, const float* init32, const double* noise,
                                  int64_t n, int64_t T, float* states_rec, float* actions_rec,
-                                 double* visited, double* final_state, void* stream) {
+                                 double* visited, double* final_state, void* workspace,
+                                 size_t workspace_bytes, void* stream) {
   if (n <= 0 || T <= 0) return 0;
   if (h0 <= 0 || h1 <= 0 || h0 > kRollMaxH || h1 > kRollMaxH || a_dim <= 0 ||
       a_dim > kRollMaxA || env_id < 0 || env_id > 1 || (env_id == 0 && !init64) ||
@@ -346,6 +527,45 @@ extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1,
   }
   const int threads = ((h0 > h1 ? h0 : h1) + 63) / 64 * 64;
   hipStream_t st = (hipStream_t)stream;
+  {
+    // several workgroups per trajectory when all of them fit on the CUs at once
+    const int np = (h1 + 63) / 64, nw = threads / 64;
+    int dev = 0, cus = 0;
+    MEPOL_HIP(hipGetDevice(&dev));
+    MEPOL_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const char* mw = getenv("MEPOL_ROLLOUT_MW");
+    if (workspace && workspace_bytes >= rollout_mw_bytes(n, h1) && h0 <= kRollMwMaxH0 &&
+        n * np <= cus && !(mw && mw[0] == '0')) {
+      char* ws = (char*)workspace;
+      int* err = (int*)ws;
+      unsigned long long* mail = (unsigned long long*)(ws + 256);
+      unsigned* flags = (unsigned*)(ws + 256 + align_up((size_t)n * 2 * np * kRollMaxA * 8, 256));
+      MEPOL_HIP(hipMemsetAsync(err, 0, sizeof(int), st));
+      MEPOL_HIP(hipMemsetAsync(flags, 0, (size_t)n * np * 4, st));
+      const size_t lds = (size_t)h0 * 64 * sizeof(double);
+#define MEPOL_ROLL_MW(E)                                                                         \
+  do {                                                                                           \
+    static bool attr = false;                                                                    \
+    if (!attr) {                                                                                 \
+      MEPOL_HIP(hipFuncSetAttribute((const void*)rollout_mlp_mw_kernel<E>,                       \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,                  \
+                                    kRollMwMaxH0 * 64 * (int)sizeof(double)));                   \
+      attr = true;                                                                               \
+    }                                                                                            \
+    hipLaunchKernelGGL((rollout_mlp_mw_kernel<E>), dim3((unsigned)(n * np)), dim3(64), lds, st, \
+                       W1, b1, h0, W2t, b2, h1, Wm, bm, log_std, a_dim, init64, init32, noise, n, \
+                       T, states_rec, actions_rec, visited, final_state, np, nw, mail, flags,    \
+                       err);                                                                     \
+  } while (0)
+      if (env_id == 0)
+        MEPOL_ROLL_MW(0);
+      else
+        MEPOL_ROLL_MW(1);
+#undef MEPOL_ROLL_MW
+      MEPOL_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   const dim3 g((unsigned)n);
   const char* kr = getenv("MEPOL_ROLLOUT_KR");
   const int want = kr ? atoi(kr) : 0;

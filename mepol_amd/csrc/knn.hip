@@ -8,18 +8,23 @@
 // ascending; ties are broken by the smaller candidate index (sklearn leaves tie order
 // implementation-defined, so this is the build's documented convention).
 //
-// Pipeline (all on one stream, no host sync, no allocation):
-//   1. pack    : candidates -> MFMA A-fragment tiles, A = [-2 c, |c|^2] (fp32), max |c|.
-//   2. select  : v_mfma_f32_32x32x2_f32 computes |c|^2 - 2 q.c for 32 candidates x 32 queries
-//                per 15-MFMA step (d = 29); each lane owns one query column and keeps a
-//                sorted top-LIST list in VGPRs, fed through a per-lane LDS buffer so the
-//                wave pays the insertion cost in batches, not per candidate.
-//   3. refine  : per query, merge the 2*split partial lists to the approximate top-LIST,
-//                recompute those distances exactly in f64, bitonic-sort by (dist, idx), and
-//                certify with a rigorous fp32 error bound that no excluded candidate can
-//                enter the top-(k+1).  Uncertified queries (near-ties across the boundary,
-//                large duplicate clusters) are queued.
-//   4. exact   : queued queries are answered by an exhaustive f64 scan (no approximation).
+// Pipeline (one stream, no allocation; one host sync for the input check):
+//   0. norms   : max |c|, max |q| and the NaN / inf / overflow counts (input validation).
+//   1. pack    : candidates scaled by a power of two sigma, A = [-2 sigma c, |sigma c|^2]
+//                rounded to f16 (the hi half only) in v_mfma_f32_32x32x16_f16 A-fragment
+//                order: one 1-KB block per (32-candidate tile, k-step of 16).
+//   2. select  : per 32-query tile (one wave) and candidate range, 2 MFMAs per k-step
+//                (A_hi x q_hi + A_hi x q_lo, f32 accumulate) give |c|^2 - 2 q.c for 32 x 32
+//                pairs; each lane owns one query column and keeps a sorted top-LIST list in
+//                VGPRs, fed through a per-lane LDS buffer (insertions paid in batches).
+//   3. refine  : per query, merge the 2*split partial lists to the approximate top-64,
+//                recompute the distances inside the selection's error band exactly in f64,
+//                bitonic-sort by (dist, idx), and certify with a rigorous bound on the f16
+//                selection's error that no excluded candidate can enter the top-(k+1).
+//                Uncertified queries (near-ties across the boundary, duplicate clusters) are
+//                queued.
+//   4. exact   : queued queries are answered by an exhaustive f64 scan (no approximation),
+//                a handful of queries spread over the whole grid (chunked scan + merge).
 #include "common.hpp"
 
 #include <algorithm>
@@ -34,58 +39,13 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
 
-constexpr float kPadNorm = 1e30f;  // |c|^2 of padding candidates: never selected
 constexpr int kBufCap = 24;        // per-lane LDS insertion buffer (entries)
 constexpr int kMaxSplit = 16;
+constexpr int kExactGrid = 512;    // blocks of the exhaustive fallback (exact_kernel)
+constexpr int kRefineList = 64;    // approximate candidates refine ranks per query (one wave)
 
 // ---------------------------------------------------------------------------------------
-// 1. pack
-// ---------------------------------------------------------------------------------------
-// apack[(t*64 + l)*KSP + s] = A[i = l&31][k = l>>5] of k-step s for candidate tile t, i.e.
-// feature f = 2s + (l>>5) of candidate c = 32t + (l&31):  f<d: -2 x_cf ; f==d: |c|^2 ; else 0.
-__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ X, int64_t n, int d,
-                                                   int KSP, int64_t nct,
-                                                   float* __restrict__ apack,
-                                                   unsigned* __restrict__ cmax_bits) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = nct * 64;
-  float mynorm = 0.f;
-  if (gid < total) {
-    const int64_t t = gid >> 6;
-    const int l = (int)(gid & 63);
-    const int h = l >> 5;
-    const int64_t c = t * 32 + (l & 31);
-    const bool valid = c < n;
-    float cn = 0.f;
-    if (valid) {
-      const float* xc = X + c * d;
-      for (int f = 0; f < d; ++f) cn = fmaf(xc[f], xc[f], cn);
-    }
-    float* dst = apack + gid * KSP;
-    for (int s = 0; s < KSP; s += 4) {
-      float v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int f = 2 * (s + u) + h;
-        float x;
-        if (valid)
-          x = (f < d) ? -2.f * X[c * d + f] : ((f == d) ? cn : 0.f);
-        else
-          x = (f == d) ? kPadNorm : 0.f;
-        v[u] = x;
-      }
-      *reinterpret_cast<float4*>(dst + s) = make_float4(v[0], v[1], v[2], v[3]);
-    }
-    if (valid && h == 0) mynorm = sqrtf(cn);
-  }
-  // wave max -> one atomic per wave (non-negative floats order like their bit patterns)
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) mynorm = fmaxf(mynorm, __shfl_xor(mynorm, m, kWave));
-  if ((threadIdx.x & 63) == 0) atomicMax(cmax_bits, __float_as_uint(mynorm));
-}
-
-// ---------------------------------------------------------------------------------------
-// 2. select
+// 2. select: list helpers
 // ---------------------------------------------------------------------------------------
 template <int LIST>
 __device__ __forceinline__ void list_insert(float (&ld)[LIST], int (&li)[LIST], float x, int xi) {
@@ -146,142 +106,8 @@ __device__ __forceinline__ void flush_buffer(float (&ld)[LIST], int (&li)[LIST],
 // Row (candidate within the tile) of accumulator register r for lane l (32x32 C/D map).
 __device__ __forceinline__ int acc_row(int r, int l) { return (r & 3) + 8 * (r >> 2) + 4 * (l >> 5); }
 
-template <int KS, int KSP, int LIST>
-__global__ __launch_bounds__(256) void select_kernel(const float* __restrict__ apack,
-                                                     const float* __restrict__ query, int64_t nq,
-                                                     int d, int64_t nct, int split,
-                                                     int64_t tiles_per_split,
-                                                     float* __restrict__ out_v,
-                                                     int* __restrict__ out_i) {
-  __shared__ float sbuf_v[4][kBufCap][64];
-  __shared__ int sbuf_i[4][kBufCap][64];
-  const int w = threadIdx.x >> 6;
-  const int l = threadIdx.x & 63;
-  const int64_t qt = (int64_t)blockIdx.x * 4 + w;
-  const int sp = blockIdx.y;
-  if (qt * 32 >= nq) return;  // wave-uniform
-  const int h = l >> 5;
-  const int64_t q = qt * 32 + (l & 31);
-  const bool qvalid = q < nq;
-
-  // B operand (queries): B[k = h][j = l&31] of step s = feature 2s + h; f == d carries 1.
-  float bq[KS];
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int f = 2 * s + h;
-    bq[s] = qvalid ? ((f < d) ? query[q * d + f] : ((f == d) ? 1.f : 0.f)) : 0.f;
-  }
-
-  // Retire the B-operand loads here and launder the registers, so no compiler-tracked load is
-  // pending inside the tile loop (otherwise its waitcnt pass drains vmcnt(0) every iteration).
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int s = 0; s < KS; ++s) asm volatile("" : "+v"(bq[s]));
-
-  float ld[LIST];
-  int li[LIST];
-#pragma unroll
-  for (int j = 0; j < LIST; ++j) {
-    ld[j] = INFINITY;
-    li[j] = -1;
-  }
-  const float thr0 = INFINITY;
-  float thr = thr0;
-  int cnt = 0;
-
-  const int64_t t0 = (int64_t)sp * tiles_per_split;
-  const int64_t t1 = min(nct, t0 + tiles_per_split);
-
-  constexpr int NV = KSP / 4;
-  const f32x4* abase = reinterpret_cast<const f32x4*>(apack + (int64_t)l * KSP);
-  // Two register buffers (ping-pong): tile t+1's loads are in flight while tile t's MFMA chain
-  // runs.  Fragment loads are issued from inline asm so the compiler's waitcnt pass (which
-  // drains to vmcnt(0) at this loop's control-flow joins) does not see them; the waits are
-  // counted by hand: the only vector-memory ops inside the loop are these NV loads per tile.
-  f32x4 A0[NV], A1[NV];
-  auto load = [&](f32x4 (&A)[NV], int64_t t) {
-    const f32x4* p = abase + t * 16 * KSP;  // 64 lanes * KSP floats = 16*KSP f32x4 per tile
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      f32x4 x;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(p + v) : "memory");
-      A[v] = x;
-    }
-  };
-  auto wait_older = [&](f32x4 (&A)[NV]) {  // all but the NV youngest loads have landed
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV) : "memory");
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      f32x4 x = A[v];
-      asm volatile("" : "+v"(x));
-      A[v] = x;
-    }
-  };
-  auto wait_all = [&](f32x4 (&A)[NV]) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      f32x4 x = A[v];
-      asm volatile("" : "+v"(x));
-      A[v] = x;
-    }
-  };
-  auto comp = [](const f32x4 (&A)[NV], int s) -> float { return A[s >> 2][s & 3]; };
-  auto tile = [&](const f32x4 (&A)[NV], int64_t t) {
-    f32x16 acc = {};
-#pragma unroll
-    for (int s = 0; s < KS; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(A, s), bq[s], acc, 0, 0, 0);
-    float m = fminf(fminf(fminf(acc[0], acc[1]), fminf(acc[2], acc[3])),
-                    fminf(fminf(acc[4], acc[5]), fminf(acc[6], acc[7])));
-    m = fminf(m, fminf(fminf(fminf(acc[8], acc[9]), fminf(acc[10], acc[11])),
-                       fminf(fminf(acc[12], acc[13]), fminf(acc[14], acc[15]))));
-    if (__ballot(m < thr)) {
-      const int base = (int)(t * 32);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (acc[r] < thr) {
-          sbuf_v[w][cnt][l] = acc[r];
-          sbuf_i[w][cnt][l] = base + acc_row(r, l);
-          ++cnt;
-        }
-      }
-      if (__ballot(cnt > kBufCap - 16)) flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0);
-    }
-  };
-  if (t0 < t1) {
-    load(A0, t0);
-    int64_t t = t0;
-#pragma nounroll
-    for (; t + 1 < t1; t += 2) {
-      load(A1, t + 1);
-      wait_older(A0);
-      tile(A0, t);
-      load(A0, min(t + 2, t1 - 1));
-      wait_older(A1);
-      tile(A1, t + 1);
-    }
-    wait_all(A0);
-    if (t < t1) tile(A0, t);
-  }
-  flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0);
-
-  if (qvalid) {
-    const int64_t o = ((q * split + sp) * 2 + h) * LIST;
-#pragma unroll
-    for (int j = 0; j < LIST; ++j) {
-      out_v[o + j] = ld[j];
-      out_i[o + j] = li[j];
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------------------
-// 2b. select on split-f16 MFMA (default): the same |c|^2 - 2 q.c, with every operand split
-//     into two f16 halves, a = a_hi + a_lo (|a - a_hi - a_lo| <= 2^-22 |a|), and the three
-//     products hi*hi + hi*lo + lo*hi accumulated in f32 by v_mfma_f32_32x32x16_f16 (exact
-//     products, f32 sums): ~f32-class accuracy at 3 MFMAs of 16x the f32 rate.  Coordinates
-//     are scaled by a power of two sigma (max norm -> (64, 128]) so |c|^2 fits f16; outputs
-//     are unscaled exactly.  refine's certification uses this path's error bound.
+// 0./1. input check, scale and pack
 // ---------------------------------------------------------------------------------------
 // max |x| over candidates (scal[0]) and over queries (scal[2]), non-negative float bit order.
 // Input validation (sklearn's check_array inside NearestNeighbors.fit / kneighbors,
@@ -333,14 +159,6 @@ __device__ __forceinline__ float knn_scale(const unsigned* __restrict__ scal) {
   return ldexpf(1.f, e);
 }
 
-// Smallest float above v (v itself for +inf / NaN).
-__device__ __forceinline__ float next_up(float v) {
-  if (!(v < INFINITY)) return v;
-  if (v == 0.f) return __uint_as_float(1u);
-  const unsigned b = __float_as_uint(v);
-  return __uint_as_float(v > 0.f ? b + 1u : b - 1u);
-}
-
 __device__ __forceinline__ void split_f16(float v, _Float16& hi, _Float16& lo) {
   hi = (_Float16)v;
   lo = (_Float16)(v - (float)hi);  // v - hi is exact in f32
@@ -350,6 +168,9 @@ constexpr float kPadNorm16 = 60000.f;  // scaled |c|^2 of padding candidates (> 
 
 // apack16[((t*64 + l)*KS16 + s)*16 + {0..7 hi, 8..15 lo}] = A[i = l&31][k = 16 s + 8 (l>>5) + j]
 // of candidate tile t: f<d: -2 sigma x_cf ; f==d: |sigma c|^2 ; else 0.
+// apack16[((t*KS16 + s)*64 + l)*8 + j] = fl16(A[i = l&31][k = 16 s + 8 (l>>5) + j]) of candidate
+// tile t, A = [-2 sigma c, |sigma c|^2, 0...]: each k-step of a tile is 1 KB, one coalesced
+// dwordx4 per lane.  Padding candidates carry a norm above every real value.
 __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X, int64_t n, int d,
                                                      int KS16, int64_t nct,
                                                      _Float16* __restrict__ apack,
@@ -370,9 +191,8 @@ __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X
       cn = fmaf(y, y, cn);
     }
   }
-  _Float16* dst = apack + gid * KS16 * 16;
   for (int s = 0; s < KS16; ++s) {
-    f16x8 hv, lv;
+    f16x8 hv;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int f = 16 * s + 8 * h + j;
@@ -381,46 +201,34 @@ __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X
         v = (f < d) ? -2.f * sg * X[c * d + f] : ((f == d) ? cn : 0.f);
       else
         v = (f == d) ? kPadNorm16 : 0.f;
-      _Float16 a, b;
-      split_f16(v, a, b);
-      hv[j] = a;
-      lv[j] = b;
+      hv[j] = (_Float16)v;
     }
-    *reinterpret_cast<f16x8*>(dst + s * 16) = hv;
-    *reinterpret_cast<f16x8*>(dst + s * 16 + 8) = lv;
+    *reinterpret_cast<f16x8*>(apack + ((t * KS16 + s) * 64 + l) * 8) = hv;
   }
 }
 
-// TAU = false: partial top-LIST lists of every query over its split's tile range, pruned from the
-//              start by the query's sampled bound tau_in (scaled units; nullptr = none).
-// TAU = true : the sampling pass.  Tiles t*tile_stride (t < nct) only, split = 1; writes
-//              tau_out[q] = the next float above min over the two half-lists of their kp1-th
-//              value: an upper bound on the query's (k+1)-th smallest approximate value over all
-//              candidates (a subset's (k+1)-th is never below the full set's), at least kp1
-//              sampled candidates lie at or below it, and the values are bitwise those of the
-//              main pass (same fragments, same MFMA chain).
-template <int KS16, int LIST, bool TAU>
+// Partial top-LIST lists of every query over its split's tile range.  The candidates are the
+// f16 hi halves of A (pack16_kernel), the queries are split into f16 hi + lo (2^-22 relative),
+// and 2 MFMAs per k-step (A_hi q_hi + A_hi q_lo) accumulate in f32: the value's error is
+// dominated by the candidate rounding, 2^-11 (|c|^2 + 2 |c||q|) (make_plan's e_terms), which
+// refine's certification accounts for.  Only the hi half travels: 1 KB per k-step and tile,
+// half the fragment stream of a split-candidate (hi + lo) selection.
+template <int KS16, int LIST>
 __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restrict__ apack,
                                                        const float* __restrict__ query,
                                                        int64_t nq, int d, int64_t nct, int split,
-                                                       int64_t tiles_per_split, int tile_stride,
-                                                       int kp1, int keep,
+                                                       int64_t tiles_per_split, int keep,
                                                        const unsigned* __restrict__ scal,
-                                                       const float* __restrict__ tau_in,
-                                                       float* __restrict__ tau_out,
                                                        float* __restrict__ out_v,
                                                        int* __restrict__ out_i) {
   __shared__ float sbuf_v[4][kBufCap][64];
   __shared__ int sbuf_i[4][kBufCap][64];
   const int w = threadIdx.x >> 6;
   const int l = threadIdx.x & 63;
-  if (TAU) keep = 0;
   // XCD-aware block mapping: workgroups go round-robin over the 8 XCDs by linear id, so with
   // sp = id % split (split a multiple of 8) every XCD only ever reads the candidate ranges
-  // sp = xcd (mod 8), which then stay resident in that XCD's 4 MB L2 instead of streaming from
-  // the Infinity Cache once per query tile.  Any other split (3 at C3) keeps the split-major
-  // order: the blocks in flight then all read one candidate range, not every range at once
-  // (the XCD mapping with split = 3 put all three ranges in every L2: 2.7x the fetch bytes).
+  // sp = xcd (mod 8), which then stay resident in that XCD's 4 MB L2.  Any other split (2 at
+  // C3) keeps the split-major order: the blocks in flight then all read one candidate range.
   const int64_t lin = (int64_t)blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
   const bool xcd_map = (split & 7) == 0;
   const int sp = xcd_map ? (int)(lin % split) : (int)blockIdx.y;
@@ -445,7 +253,8 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
       bhi[s][j] = a;
       blo[s][j] = b;
     }
-  float thr0 = (!TAU && tau_in && qvalid) ? tau_in[q] : INFINITY;
+  // Retire the B-operand loads here and launder the registers, so no compiler-tracked load is
+  // pending inside the tile loop (otherwise its waitcnt pass drains vmcnt(0) every iteration).
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
   for (int s = 0; s < KS16; ++s) {
@@ -455,7 +264,6 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
     bhi[s] = __builtin_bit_cast(f16x8, x);
     blo[s] = __builtin_bit_cast(f16x8, y);
   }
-  asm volatile("" : "+v"(thr0));  // retired above (see filter16_kernel)
 
   float ld[LIST];
   int li[LIST];
@@ -464,28 +272,29 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
     ld[j] = INFINITY;
     li[j] = -1;
   }
+  const float thr0 = INFINITY;
   float thr = thr0;
   int cnt = 0;
 
   const int64_t t0 = (int64_t)sp * tiles_per_split;
   const int64_t t1 = min(nct, t0 + tiles_per_split);
 
-  // Three fragment buffers: tile t's MFMAs run while tile t-1's threshold work executes and
-  // tile t+1's loads are in flight; a buffer is refilled (tile t+2) only after the chain that
-  // read it has completed (its results were consumed).  Loads are inline asm with hand-counted
-  // waits (NV per tile; no other vector-memory op in the loop).
-  constexpr int NV = 2 * KS16;  // dwordx4 per lane per tile: hi and lo halves of each k-step
-  // Fragment buffers: three for KS16 <= 3; two for KS16 = 4 (d + 1 <= 64, HandReach), whose
-  // 8-register-per-k-step buffers would otherwise put the kernel at the 256-VGPR cap.
-  constexpr int NB = KS16 >= 4 ? 2 : 3;
-  const f32x4* abase = reinterpret_cast<const f32x4*>(apack) + (int64_t)l * NV;
+  // Fragment buffers in registers: tile t's MFMAs run while tile t-1's threshold work executes
+  // and the next tiles' loads are in flight; a buffer is refilled only after the chain that
+  // read it has completed.  Loads are inline asm with hand-counted waits (NV per tile; no other
+  // vector-memory op in the loop).  Three buffers, two where a 4-k-step tile and long lists
+  // would otherwise reach the 256-VGPR cap (at the cap the asm-load buffers are not safe from
+  // register copies).
+  constexpr int NV = KS16;  // dwordx4 per lane per tile: one per k-step
+  constexpr int NB = (KS16 >= 4 && LIST > 32) ? 2 : 3;
+  const f32x4* abase = reinterpret_cast<const f32x4*>(apack) + l;
   f32x4 Bf[NB][NV];
   auto load = [&](f32x4 (&A)[NV], int64_t t) {
-    const f32x4* p = abase + t * tile_stride * 64 * NV;
+    const f32x4* p = abase + t * 64 * NV;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       f32x4 x;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(p + v) : "memory");
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(p + v * 64) : "memory");
       A[v] = x;
     }
   };
@@ -502,11 +311,9 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
     f32x16 acc = {};
 #pragma unroll
     for (int s = 0; s < KS16; ++s) {
-      const f16x8 ah = __builtin_bit_cast(f16x8, A[2 * s]);
-      const f16x8 al = __builtin_bit_cast(f16x8, A[2 * s + 1]);
+      const f16x8 ah = __builtin_bit_cast(f16x8, A[s]);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bhi[s], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, blo[s], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bhi[s], acc, 0, 0, 0);
     }
     return acc;
   };
@@ -516,7 +323,7 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
     m = fminf(m, fminf(fminf(fminf(acc[8], acc[9]), fminf(acc[10], acc[11])),
                        fminf(fminf(acc[12], acc[13]), fminf(acc[14], acc[15]))));
     if (__ballot(m < thr)) {
-      const int base = (int)(t * tile_stride * 32);
+      const int base = (int)(t * 32);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         if (acc[r] < thr) {
@@ -609,17 +416,6 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
   }
   flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0, keep);
 
-  if (TAU) {
-    // each half keeps its m = ceil(kp1/2) smallest; the union then holds 2m >= kp1 sampled
-    // values <= max of the two m-th values, a bound about as tight as the union's kp1-th
-    const int m = (kp1 + 1) / 2;
-    float v = INFINITY;
-#pragma unroll
-    for (int j = 0; j < LIST; ++j) v = (j == m - 1) ? ld[j] : v;
-    v = fmaxf(v, __shfl_xor(v, 32, kWave));
-    if (qvalid && h == 0) tau_out[q] = next_up(v);
-    return;
-  }
   if (qvalid) {
     // The last slot carries this lane's final bound: every candidate of its range that is not
     // in the list has an approximate value >= min(list last, thr) (rejected against thr, or
@@ -635,172 +431,6 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
     out_v[o + LIST - 1] = bound * inv_s2;
     out_i[o + LIST - 1] = (bound < ld[LIST - 1]) ? -1 : li[LIST - 1];
   }
-}
-
-// 2c. filter pass (split-f16, seeded by the sampling pass): no sorted lists at all.  Every
-//     candidate whose approximate value is below the query's sampled bound tau (scaled units) is
-//     appended to a per-lane LDS buffer; full buffers are spilled to the query's survivor array
-//     (capacity cap, global count per query; entries past cap only raise the count, which makes
-//     refine queue the query for the exhaustive path).  The tile loop is MFMA chain + min tree +
-//     one compare per tile; with no lists in registers the accumulators stay in VGPRs.
-template <int KS16>
-__global__ __launch_bounds__(256) void filter16_kernel(const _Float16* __restrict__ apack,
-                                                       const float* __restrict__ query,
-                                                       int64_t nq, int d, int64_t nct, int split,
-                                                       int64_t tiles_per_split,
-                                                       const unsigned* __restrict__ scal,
-                                                       const float* __restrict__ tau, int cap,
-                                                       int* __restrict__ counts,
-                                                       float* __restrict__ sv,
-                                                       int* __restrict__ si) {
-  __shared__ float sbuf_v[4][kBufCap][64];
-  __shared__ int sbuf_i[4][kBufCap][64];
-  const int w = threadIdx.x >> 6;
-  const int l = threadIdx.x & 63;
-  // XCD-aware block mapping (see select16_kernel)
-  const int64_t lin = (int64_t)blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
-  const int sp = (int)(lin % split);
-  const int64_t qt = (lin / split) * 4 + w;
-  if (qt * 32 >= nq) return;  // wave-uniform
-  const int h = l >> 5;
-  const int64_t q = qt * 32 + (l & 31);
-  const bool qvalid = q < nq;
-  const float sg = knn_scale(scal);
-  const float inv_s2 = 1.f / (sg * sg);
-
-  f16x8 bhi[KS16], blo[KS16];
-#pragma unroll
-  for (int s = 0; s < KS16; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int f = 16 * s + 8 * h + j;
-      const float v = qvalid ? ((f < d) ? sg * query[q * d + f] : ((f == d) ? 1.f : 0.f)) : 0.f;
-      _Float16 a, b;
-      split_f16(v, a, b);
-      bhi[s][j] = a;
-      blo[s][j] = b;
-    }
-  float thr = qvalid ? tau[q] : -INFINITY;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int s = 0; s < KS16; ++s) {
-    f32x4 x = __builtin_bit_cast(f32x4, bhi[s]);
-    f32x4 y = __builtin_bit_cast(f32x4, blo[s]);
-    asm volatile("" : "+v"(x), "+v"(y));
-    bhi[s] = __builtin_bit_cast(f16x8, x);
-    blo[s] = __builtin_bit_cast(f16x8, y);
-  }
-  // retired by the wait above: no compiler-tracked load may reach the loop (it would drain
-  // vmcnt(0) at the first use in every iteration and serialise the fragment pipeline)
-  asm volatile("" : "+v"(thr));
-  int cnt = 0;
-  const int64_t t0 = (int64_t)sp * tiles_per_split;
-  const int64_t t1 = min(nct, t0 + tiles_per_split);
-
-  constexpr int NV = 2 * KS16;
-  const f32x4* abase = reinterpret_cast<const f32x4*>(apack) + (int64_t)l * NV;
-  f32x4 Bf[3][NV];
-  auto load = [&](f32x4 (&A)[NV], int64_t t) {
-    const f32x4* p = abase + t * 64 * NV;
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      f32x4 x;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(p + v) : "memory");
-      A[v] = x;
-    }
-  };
-  auto landed = [&](f32x4 (&A)[NV]) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV) : "memory");
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      f32x4 x = A[v];
-      asm volatile("" : "+v"(x));
-      A[v] = x;
-    }
-  };
-  auto chain = [&](const f32x4 (&A)[NV]) -> f32x16 {
-    f32x16 acc = {};
-#pragma unroll
-    for (int s = 0; s < KS16; ++s) {
-      const f16x8 ah = __builtin_bit_cast(f16x8, A[2 * s]);
-      const f16x8 al = __builtin_bit_cast(f16x8, A[2 * s + 1]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bhi[s], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, blo[s], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bhi[s], acc, 0, 0, 0);
-    }
-    return acc;
-  };
-  // Spill this lane's buffer to the query's survivor array.  The returning atomic makes the
-  // compiler drain vmcnt, which also retires the in-flight fragment loads (correct, and rare).
-  auto spill = [&]() {
-    if (cnt > 0) {
-      const int base = atomicAdd(counts + q, cnt);
-      for (int e = 0; e < cnt; ++e) {
-        const int pos = base + e;
-        if (pos < cap) {
-          sv[q * cap + pos] = sbuf_v[w][e][l] * inv_s2;
-          si[q * cap + pos] = sbuf_i[w][e][l];
-        }
-      }
-    }
-    cnt = 0;
-    // vmcnt(0) here, visible to the compiler: its stores are complete on this rare path, so
-    // the loop latch needs no drain of its own (which would serialise every tile's loads)
-    __builtin_amdgcn_s_waitcnt(0x0F70);
-  };
-  auto process = [&](f32x16 acc, int64_t t) {
-    const float m = fminf(
-        fminf(fminf(fminf(acc[0], acc[1]), fminf(acc[2], acc[3])),
-              fminf(fminf(acc[4], acc[5]), fminf(acc[6], acc[7]))),
-        fminf(fminf(fminf(acc[8], acc[9]), fminf(acc[10], acc[11])),
-              fminf(fminf(acc[12], acc[13]), fminf(acc[14], acc[15]))));
-    if (__ballot(m < thr)) {
-      const int base = (int)(t * 32);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (acc[r] < thr) {
-          sbuf_v[w][cnt][l] = acc[r];
-          sbuf_i[w][cnt][l] = base + acc_row(r, l);
-          ++cnt;
-        }
-      }
-      if (__ballot(cnt > kBufCap - 16)) spill();
-    }
-  };
-  if (t0 < t1) {
-    const int64_t tl = t1 - 1;
-    load(Bf[0], t0);
-    load(Bf[1], min(t0 + 1, tl));
-    landed(Bf[0]);
-    f32x16 accP = chain(Bf[0]);
-    load(Bf[2], min(t0 + 2, tl));
-    int64_t t = t0 + 1;
-#define MEPOL_FLT16_STEP(CUR, PREV)         \
-  {                                         \
-    landed(Bf[CUR]);                        \
-    const f32x16 accN = chain(Bf[CUR]);     \
-    process(accP, t - 1);                   \
-    load(Bf[PREV], min(t + 2, tl));         \
-    accP = accN;                            \
-    ++t;                                    \
-  }
-#pragma nounroll
-    while (t + 2 < t1) {
-      MEPOL_FLT16_STEP(1, 0)
-      MEPOL_FLT16_STEP(2, 1)
-      MEPOL_FLT16_STEP(0, 2)
-    }
-    if (t < t1) MEPOL_FLT16_STEP(1, 0)
-    if (t < t1) MEPOL_FLT16_STEP(2, 1)
-#undef MEPOL_FLT16_STEP
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int b = 0; b < 3; ++b)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[b][v]));
-    process(accP, t - 1);
-  }
-  spill();
 }
 
 // ---------------------------------------------------------------------------------------
@@ -857,9 +487,8 @@ __device__ __forceinline__ double sqrt_rn(double x) {
 template <int LIST, int MAXP>
 __global__ __launch_bounds__(256) void refine_kernel(
     const float* __restrict__ cand, int64_t nc, const float* __restrict__ query, int64_t nq, int d,
-    int kp1, int M, int list_len, const int* __restrict__ counts,
-    const float* __restrict__ lists_v, const int* __restrict__ lists_i,
-    const unsigned* __restrict__ cmax_bits, int e_terms, const float* __restrict__ tau,
+    int kp1, int M, int list_len, const float* __restrict__ lists_v,
+    const int* __restrict__ lists_i, const unsigned* __restrict__ cmax_bits, int e_terms,
     double* __restrict__ Dout,
     int64_t* __restrict__ I64, int32_t* __restrict__ I32, int* __restrict__ flag_count,
     int* __restrict__ flag_list, int rank_merge) {
@@ -879,23 +508,15 @@ __global__ __launch_bounds__(256) void refine_kernel(
   const int64_t qb = xcd * per + min(xcd, rem) + (bx >> 3);
   const int64_t q = qb * 4 + w;
   if (q >= nq) return;
-  // Candidate entries of this query: M per query.  Lists mode (counts == nullptr): 2*split
-  // ascending partial lists of list_len each.  Survivor mode: counts[q] unsorted entries (a count
-  // above M means entries were dropped: the query is not certified).
+  // Candidate entries of this query: 2*split ascending partial lists of list_len each, the last
+  // slot of each carrying that lane's prune bound (select16_kernel).
   const float* lv = lists_v + q * M;
   const int* lix = lists_i + q * M;
-  const int nval = counts ? min(counts[q], M) : M;
-  const bool overflow = counts && counts[q] > M;
+  const int nval = M;
 
-  // Bound part 1: min over partial lists of their maxima (last, lists are ascending) and the
-  // sampled bound the selection started from (scaled units -> unscaled, exact power of two).
+  // Bound part 1: min over partial lists of their last slot (their lanes' final bounds).
   float bnd = INFINITY;
-  if (tau) {
-    const float sg = knn_scale(cmax_bits);
-    bnd = tau[q] / (sg * sg);
-  }
-  if (list_len > 0)
-    for (int p = l; p < M / list_len; p += 64) bnd = fminf(bnd, lv[p * list_len + list_len - 1]);
+  for (int p = l; p < M / list_len; p += 64) bnd = fminf(bnd, lv[p * list_len + list_len - 1]);
 
   float ev[MAXP];
   int ei[MAXP];
@@ -989,8 +610,8 @@ __global__ __launch_bounds__(256) void refine_kernel(
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) qn2 += __shfl_xor(qn2, m, kWave);
   const double cmax = (double)__uint_as_float(*cmax_bits);
-  // e_terms * 2^-24 * (C^2 + 2 C |q|) bounds the selection's error (f32 path: 4 (d + 1);
-  // split-f16 path: 2 (3 K + 16 + d), see make_plan), C = max candidate norm.
+  // e_terms * 2^-24 * (C^2 + 2 C |q|) bounds the selection's error (make_plan), C = max
+  // candidate norm.
   const double E = (double)e_terms * 5.9604644775390625e-08 *
                        (cmax * cmax + 2.0 * cmax * sqrt(qn2)) + 1e-300;
   // Rank merge: only the candidates within the error band of the (k+1)-th approximate value
@@ -1040,7 +661,7 @@ __global__ __launch_bounds__(256) void refine_kernel(
   // d^2 >= bnd + |q|^2 - E.
   const double ek = __shfl(dd, kp1 - 1, kWave);
   const int eki = __shfl(di, kp1 - 1, kWave);
-  bool ok = (eki != INT_MAX) && !overflow;
+  bool ok = eki != INT_MAX;
   if (bnd < 1e29f) ok = ok && (ek < ((double)bnd + qn2) - E);
   if (l < kp1) {
     Dout[q * kp1 + l] = sqrt_rn(dd);
@@ -1056,6 +677,87 @@ __global__ __launch_bounds__(256) void refine_kernel(
 // ---------------------------------------------------------------------------------------
 // 4. exhaustive exact fallback for uncertified queries
 // ---------------------------------------------------------------------------------------
+// Exhaustive f64 top-kp1 of query xq over candidates [c0, c1), lexicographic (dist, idx):
+// per-thread sorted lists, then kp1 rounds of block argmin; round r's winner goes to
+// emit(r, d, i) on thread 0 (i = INT_MAX, d = inf when the range holds fewer than kp1).
+template <int LIST, typename Emit>
+__device__ __forceinline__ void exact_scan(const float* __restrict__ cand, int64_t c0, int64_t c1,
+                                           const float* __restrict__ xq, int d, int kp1,
+                                           double* red_d, int* red_i, Emit emit) {
+  const int tid = threadIdx.x;
+  const int l = tid & 63, w = tid >> 6;
+  double ld[LIST];
+  int li[LIST];
+#pragma unroll
+  for (int j = 0; j < LIST; ++j) {
+    ld[j] = INFINITY;
+    li[j] = INT_MAX;
+  }
+#pragma nounroll
+  for (int64_t c = c0 + tid; c < c1; c += blockDim.x) {
+    const double x = exact_d2(xq, cand + c * d, d);
+    const int xi = (int)c;
+    if (lex_less(x, xi, ld[LIST - 1], li[LIST - 1])) {
+      bool cc[LIST];
+#pragma unroll
+      for (int j = 0; j < LIST; ++j) cc[j] = lex_less(x, xi, ld[j], li[j]);
+#pragma unroll
+      for (int j = LIST - 1; j >= 1; --j) {
+        ld[j] = cc[j - 1] ? ld[j - 1] : (cc[j] ? x : ld[j]);
+        li[j] = cc[j - 1] ? li[j - 1] : (cc[j] ? xi : li[j]);
+      }
+      ld[0] = cc[0] ? x : ld[0];
+      li[0] = cc[0] ? xi : li[0];
+    }
+  }
+#pragma nounroll
+  for (int r = 0; r < kp1; ++r) {
+    double bd = ld[0];
+    int bi = li[0];
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      const double od = __shfl_xor(bd, m, kWave);
+      const int oi = __shfl_xor(bi, m, kWave);
+      if (lex_less(od, oi, bd, bi)) {
+        bd = od;
+        bi = oi;
+      }
+    }
+    if (l == 0) {
+      red_d[w] = bd;
+      red_i[w] = bi;
+    }
+    __syncthreads();
+    bd = red_d[0];
+    bi = red_i[0];
+#pragma unroll
+    for (int u = 1; u < 4; ++u)
+      if (lex_less(red_d[u], red_i[u], bd, bi)) {
+        bd = red_d[u];
+        bi = red_i[u];
+      }
+    __syncthreads();
+    if (li[0] == bi && bi != INT_MAX) {
+#pragma unroll
+      for (int j = 0; j < LIST - 1; ++j) {
+        ld[j] = ld[j + 1];
+        li[j] = li[j + 1];
+      }
+      ld[LIST - 1] = INFINITY;
+      li[LIST - 1] = INT_MAX;
+    }
+    if (tid == 0) emit(r, bd, bi);
+  }
+}
+
+// Queued (uncertified) queries.  With fewer queries than blocks each query's candidates are cut
+// into nchunk = grid / count ranges, one block each (partial top-kp1 lists to part_*, merged by
+// exact_merge_kernel): a handful of queries then use the whole chip instead of one CU each.
+// With part_d == nullptr or count >= grid, a block answers whole queries.
+__host__ __device__ inline int exact_nchunk(int count, int grid) {
+  return (count <= 0 || count >= grid) ? 1 : grid / count;
+}
+
 template <int LIST>
 __global__ __launch_bounds__(256) void exact_kernel(const float* __restrict__ cand, int64_t nc,
                                                     const float* __restrict__ query, int64_t nq,
@@ -1064,81 +766,110 @@ __global__ __launch_bounds__(256) void exact_kernel(const float* __restrict__ ca
                                                     const int* __restrict__ flag_list,
                                                     double* __restrict__ Dout,
                                                     int64_t* __restrict__ I64,
-                                                    int32_t* __restrict__ I32) {
+                                                    int32_t* __restrict__ I32,
+                                                    double* __restrict__ part_d,
+                                                    int* __restrict__ part_i) {
   __shared__ double red_d[4];
   __shared__ int red_i[4];
-  const int tid = threadIdx.x;
-  const int l = tid & 63, w = tid >> 6;
   const int count = *flag_count;
-  for (int fi = blockIdx.x; fi < count; fi += gridDim.x) {
-    const int64_t q = flag_list[fi];
-    const float* xq = query + q * d;
-    double ld[LIST];
-    int li[LIST];
-#pragma unroll
-    for (int j = 0; j < LIST; ++j) {
-      ld[j] = INFINITY;
-      li[j] = INT_MAX;
+  const int nchunk = part_d ? exact_nchunk(count, (int)gridDim.x) : 1;
+  if (nchunk == 1) {
+    for (int fi = blockIdx.x; fi < count; fi += gridDim.x) {
+      const int64_t q = flag_list[fi];
+      exact_scan<LIST>(cand, 0, nc, query + q * d, d, kp1, red_d, red_i,
+                       [&](int r, double bd, int bi) {
+                         Dout[q * kp1 + r] = sqrt_rn(bd);
+                         if (I64) I64[q * kp1 + r] = bi;
+                         if (I32) I32[(int64_t)r * nq + q] = bi;  // transposed [kp1][nq]
+                       });
     }
-#pragma nounroll
-    for (int64_t c = tid; c < nc; c += blockDim.x) {
-      const double x = exact_d2(xq, cand + c * d, d);
-      const int xi = (int)c;
-      if (lex_less(x, xi, ld[LIST - 1], li[LIST - 1])) {
-        bool cc[LIST];
+    return;
+  }
+  const int fi = (int)blockIdx.x / nchunk, ch = (int)blockIdx.x % nchunk;
+  if (fi >= count) return;
+  const int64_t q = flag_list[fi];
+  const int64_t c0 = nc * ch / nchunk, c1 = nc * (ch + 1) / nchunk;
+  const int64_t o = ((int64_t)fi * nchunk + ch) * kp1;
+  exact_scan<LIST>(cand, c0, c1, query + q * d, d, kp1, red_d, red_i,
+                   [&](int r, double bd, int bi) {
+                     part_d[o + r] = bd;
+                     part_i[o + r] = bi;
+                   });
+}
+
+// Merge of the nchunk sorted partial lists of one queued query (exact_kernel, chunked form):
+// kp1 rounds of block argmin over the list heads; grid = the exact kernel's grid.
+__global__ __launch_bounds__(256) void exact_merge_kernel(int grid, int kp1, int64_t nq,
+                                                          const int* __restrict__ flag_count,
+                                                          const int* __restrict__ flag_list,
+                                                          const double* __restrict__ part_d,
+                                                          const int* __restrict__ part_i,
+                                                          double* __restrict__ Dout,
+                                                          int64_t* __restrict__ I64,
+                                                          int32_t* __restrict__ I32) {
+  __shared__ double red_d[4];
+  __shared__ int red_i[4];
+  __shared__ int red_t[4];
+  const int count = *flag_count;
+  const int nchunk = exact_nchunk(count, grid);
+  const int fi = blockIdx.x;
+  if (nchunk == 1 || fi >= count) return;
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int64_t q = flag_list[fi];
+  const int64_t base = (int64_t)fi * nchunk * kp1;
+  constexpr int kPer = 2;  // lists per thread: nchunk <= grid <= 512
+  int pos[kPer] = {0, 0};
+  for (int r = 0; r < kp1; ++r) {
+    double bd = INFINITY;
+    int bi = INT_MAX, bt = -1;
 #pragma unroll
-        for (int j = 0; j < LIST; ++j) cc[j] = lex_less(x, xi, ld[j], li[j]);
-#pragma unroll
-        for (int j = LIST - 1; j >= 1; --j) {
-          ld[j] = cc[j - 1] ? ld[j - 1] : (cc[j] ? x : ld[j]);
-          li[j] = cc[j - 1] ? li[j - 1] : (cc[j] ? xi : li[j]);
+    for (int u = 0; u < kPer; ++u) {
+      const int ch = tid + u * 256;
+      if (ch < nchunk && pos[u] < kp1) {
+        const double x = part_d[base + (int64_t)ch * kp1 + pos[u]];
+        const int xi = part_i[base + (int64_t)ch * kp1 + pos[u]];
+        if (lex_less(x, xi, bd, bi)) {
+          bd = x;
+          bi = xi;
+          bt = u;
         }
-        ld[0] = cc[0] ? x : ld[0];
-        li[0] = cc[0] ? xi : li[0];
       }
     }
-    // kp1 rounds of block argmin over list heads; the winner pops its head.
-#pragma nounroll
-    for (int r = 0; r < kp1; ++r) {
-      double bd = ld[0];
-      int bi = li[0];
+    int owner = bt >= 0 ? tid * kPer + bt : INT_MAX;  // which (thread, list) holds the winner
 #pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) {
-        const double od = __shfl_xor(bd, m, kWave);
-        const int oi = __shfl_xor(bi, m, kWave);
-        if (lex_less(od, oi, bd, bi)) {
-          bd = od;
-          bi = oi;
-        }
+    for (int m = 32; m >= 1; m >>= 1) {
+      const double od = __shfl_xor(bd, m, kWave);
+      const int oi = __shfl_xor(bi, m, kWave);
+      const int ot = __shfl_xor(owner, m, kWave);
+      if (lex_less(od, oi, bd, bi) || (od == bd && oi == bi && ot < owner)) {
+        bd = od;
+        bi = oi;
+        owner = ot;
       }
-      if (l == 0) {
-        red_d[w] = bd;
-        red_i[w] = bi;
-      }
-      __syncthreads();
-      bd = red_d[0];
-      bi = red_i[0];
+    }
+    if (l == 0) {
+      red_d[w] = bd;
+      red_i[w] = bi;
+      red_t[w] = owner;
+    }
+    __syncthreads();
+    bd = red_d[0];
+    bi = red_i[0];
+    owner = red_t[0];
 #pragma unroll
-      for (int u = 1; u < 4; ++u)
-        if (lex_less(red_d[u], red_i[u], bd, bi)) {
-          bd = red_d[u];
-          bi = red_i[u];
-        }
-      __syncthreads();
-      if (li[0] == bi) {
-#pragma unroll
-        for (int j = 0; j < LIST - 1; ++j) {
-          ld[j] = ld[j + 1];
-          li[j] = li[j + 1];
-        }
-        ld[LIST - 1] = INFINITY;
-        li[LIST - 1] = INT_MAX;
+    for (int u = 1; u < 4; ++u)
+      if (lex_less(red_d[u], red_i[u], bd, bi) ||
+          (red_d[u] == bd && red_i[u] == bi && red_t[u] < owner)) {
+        bd = red_d[u];
+        bi = red_i[u];
+        owner = red_t[u];
       }
-      if (tid == 0) {
-        Dout[q * kp1 + r] = sqrt_rn(bd);
-        if (I64) I64[q * kp1 + r] = bi;
-        if (I32) I32[(int64_t)r * nq + q] = bi;  // transposed [kp1][nq]
-      }
+    __syncthreads();
+    if (owner != INT_MAX && owner / kPer == tid) ++pos[owner % kPer];
+    if (tid == 0) {
+      Dout[q * kp1 + r] = sqrt_rn(bd);
+      if (I64) I64[q * kp1 + r] = bi;
+      if (I32) I32[(int64_t)r * nq + q] = bi;  // transposed [kp1][nq]
     }
   }
 }
@@ -1153,23 +884,17 @@ __global__ void fill_identity_kernel(int* s, int64_t n) {
 // host-side plan + dispatch
 // ---------------------------------------------------------------------------------------
 struct Plan {
-  int d, kp1, KS, KSP, LIST, split, maxp;
-  int mode;       // 0: f32 MFMA selection, 1: split-f16 MFMA selection (default, d + 1 <= 64)
-  int KS16;       // k-steps of 16 (mode 1)
+  int d, kp1, LIST, split, maxp;
+  int KS16;       // k-steps of 16: ceil((d + 1) / 16) <= 4
   int e_terms;    // selection error bound multiplier (refine certification)
-  int sample;     // mode 1: tile stride of the sampling pass that seeds each query's bound (0: off)
-  int filter;     // mode 1 + sampling: survivor filter pass (filter16_kernel) instead of lists
-  int tau_list;   // list length of the sampling pass: >= ceil(kp1 / 2)
-  int keep;       // split-f16 lists: per-half entries behind the union prune bound (0: off)
-  int LIST16;     // split-f16 select: per-half list length (refine keeps LIST >= kp1 + 4)
-  int M;          // refine input entries per query (lists: 2*split*LIST; filter: capacity)
-  int list_len;   // refine: length of each ascending partial list (0: unsorted survivors)
+  int keep;       // per-half entries behind the union prune bound
+  int LIST16;     // per-half select list length
+  int M;          // refine input entries per query: 2*split*LIST16
   int64_t nc, nq, nct, nqt, tiles_per_split;
-  size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_tau, off_cnt, total;
+  size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_part, total;
 };
 
-static const int kKSChoices[] = {2, 4, 8, 12, 15, 16, 24, 32};
-static const int kListChoices[] = {8, 16, 24, 32, 40, 64};
+static const int kListChoices[] = {8, 16, 24, 32, 40};
 
 static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Plan* P) {
   if (nc <= 0 || nq < 0 || d <= 0 || kp1 <= 0) {
@@ -1186,107 +911,53 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
     set_error("mepol_knn: n_cand=%lld exceeds int32 indexing", (long long)nc);
     return kErrUnsupported;
   }
-  const int need_ks = (d + 1 + 1) / 2;
-  int KS = -1;
-  for (int v : kKSChoices)
-    if (v >= need_ks) {
-      KS = v;
-      break;
-    }
-  int LIST = -1;
-  for (int v : kListChoices)
-    if (v >= kp1 + 4 || (v == 64 && kp1 <= 60)) {
-      LIST = v;
-      break;
-    }
-  if (KS < 0 || LIST < 0) {
-    set_error("mepol_knn: unsupported d=%d / k+1=%d (fast path supports d<=63, k+1<=60)", d, kp1);
+  if (d > 63 || kp1 > 60) {
+    set_error("mepol_knn: unsupported d=%d / k+1=%d (fast path supports d<=63, k+1<=60; "
+              "mepol_knn_exact covers the rest)", d, kp1);
     return kErrUnsupported;
   }
   P->d = d;
   P->kp1 = kp1;
-  {
-    const char* prec = getenv("MEPOL_KNN_PRECISION");
-    const bool want_f32 = prec && (prec[0] == 'f' && prec[1] == '3' && prec[2] == '2');
-    P->KS16 = (d + 1 + 15) / 16;
-    // split-f16 lists: each half-lane keeps LIST16 entries and prunes against the union bound
-    // (flush_buffer, keep = ceil(kp1/2) + 2 per half: 2 keep >= kp1 + 3).  A half holding more
-    // than LIST16 of the query's nearest candidates only costs certification (exact path).
-    P->keep = (kp1 + 1) / 2 + 2;
-    P->LIST16 = 64;
-    for (int v : kListChoices)
-      if (v >= P->keep + 4) {
-        P->LIST16 = v;
-        break;
-      }
-    // split-f16 instantiations that stay below the 256-VGPR cap (at the cap the fragment
-    // buffers of the asm-load pipeline are no longer safe from register copies)
-    // (<3, 40> and every KS16 = 4 list size needed for kp1 > 21 reach the cap: excluded)
-    // KS16 = 4 runs a double-buffered pipeline (select16_kernel, NB = 2) with lists <= 32
-    const bool fits = (P->KS16 <= 3 && P->LIST16 <= (P->KS16 == 3 ? 32 : 40)) ||
-                      (P->KS16 == 4 && P->LIST16 <= 32);
-    P->mode = (!want_f32 && fits) ? 1 : 0;
-    // f32: d + 1 fma-chain roundings, x4 margin.  split-f16: 3 K products per output summed in
-    // f32 (<= 3K roundings), operand splitting 3 * 2^-22 = 12 * 2^-24, |c|^2 in f32 (d), x2.
-    P->e_terms = P->mode ? 2 * (3 * 16 * P->KS16 + 16 + d) : 4 * (d + 1);
-    // Sampling pass: every S-th candidate tile (MEPOL_KNN_SAMPLE=S, off by default: at C3 the
-    // survivor filter measured slower than the list selection); only worth it when the sample
-    // still holds many tiles.
-    const char* smp = getenv("MEPOL_KNN_SAMPLE");
-    int S = smp ? atoi(smp) : 0;
-    const int64_t nct = (nc + 31) / 32;
-    if (S < 2 || P->mode != 1 || P->KS16 > 3 || nct / S < 8 || (int64_t)32 * (nct / S) < 4 * kp1)
-      S = 0;
-    P->sample = S;
-    P->tau_list = 64;
-    for (int v : kListChoices)
-      if (v >= (kp1 + 1) / 2) {
-        P->tau_list = v;
-        break;
-      }
-    const char* flt = getenv("MEPOL_KNN_FILTER");
-    P->filter = (S > 0 && !(flt && flt[0] == '0')) ? 1 : 0;
-  }
-  P->KS = KS;
-  P->KSP = (KS + 3) / 4 * 4;
-  if (P->mode != 1 || P->filter) P->keep = 0;
-  P->LIST = LIST;
+  P->KS16 = (d + 1 + 15) / 16;
+  // f16 lists: each half-lane keeps LIST16 entries and prunes against the union bound
+  // (flush_buffer, keep = ceil(kp1/2) + 2 per half: 2 keep >= kp1 + 3).  A half holding more
+  // than LIST16 of the query's nearest candidates only costs certification (exact path).
+  P->keep = (kp1 + 1) / 2 + 2;
+  P->LIST16 = 40;
+  for (int v : kListChoices)
+    if (v >= P->keep + 4) {
+      P->LIST16 = v;
+      break;
+    }
+  // Selection error bound E = e_terms * 2^-24 * (C^2 + 2 C |q|), unscaled, C = max candidate
+  // norm: the f16 rounding of -2 sigma c and of |sigma c|^2 (2^-11 = 2^13 * 2^-24 relative
+  // each: 2^-11 (2 |c||q| + |c|^2)), the query split (2^-22), the 2 K products per output
+  // summed in f32 (<= 2K roundings) and |c|^2 in f32 (d roundings), these small terms x2, and
+  // 64 for the f16 subnormal range.
+  P->e_terms = 8192 + 64 + 2 * (2 * 16 * P->KS16 + 16 + d);
+  // the selection's error band (~0.1 at C3) holds a few more candidates around the (k+1)-th
+  // than kp1 + 4: refine ranks the approximate top 64 and evaluates those inside the band
+  P->LIST = kRefineList;
   P->nc = nc;
   P->nq = nq;
   P->nct = (nc + 31) / 32;
   P->nqt = (nq + 31) / 32;
   int split = split_hint;
-  if (split <= 0 && P->mode == 1 && P->filter) {
-    // filter pass: 8 candidate ranges, one per XCD (filter16's block mapping), each small
-    // enough for that XCD's L2 (25.6 MB of fragments at C3 -> 3.2 MB per XCD)
-    split = 8;
-    while (split > 1 && P->nct / split < 16) split >>= 1;
-  } else if (split <= 0) {
+  if (split <= 0) {
     // enough waves to fill 256 CUs x 2 waves/SIMD several times over, tiles >= 16 per split.
     // Every (query, split) pays the list warm-up (the prune bound starts at +inf), so fewer,
-    // longer ranges win once the chip is full: C3 split 2 = 12.9 ms, 3 = 13.4, 8 = 17.2
-    // (tools/knn_splits.sh).  The split-f16 lists keep >= 2 ranges (one range of 24-entry half
-    // lists certifies too few queries).
-    const int64_t target = P->mode == 1 ? 12500 : 16384;
-    split = (int)std::min<int64_t>(kMaxSplit, std::max<int64_t>(1, (target + P->nqt - 1) / std::max<int64_t>(P->nqt, 1)));
-    if (P->mode == 1) split = std::max(split, 2);
+    // longer ranges win once the chip is full (tools/knn_splits.sh).  The lists keep >= 2
+    // ranges (one range of half lists certifies too few queries).
+    const int64_t target = 12500;
+    split = (int)std::min<int64_t>(kMaxSplit, std::max<int64_t>(1, (target + P->nqt - 1) /
+                                                                      std::max<int64_t>(P->nqt, 1)));
+    split = std::max(split, 2);
     while (split > 1 && P->nct / split < 16) --split;
   }
   split = std::max(1, std::min(split, kMaxSplit));
   P->split = split;
   P->tiles_per_split = (P->nct + split - 1) / split;
-  if (P->filter) {
-    // survivors of the sampled bound: ~S*kp1 expected per query (S = 16 -> ~500 at k+1 = 31),
-    // capacity 32*kp1 (>= 256); an overflowing query is answered by the exhaustive path
-    const char* capv = getenv("MEPOL_KNN_CAP");
-    const int cap = capv ? atoi(capv) : 32 * kp1;
-    P->M = (int)align_up((size_t)std::max(256, std::min(cap, 2048)), 64);
-    P->list_len = 0;
-  } else {
-    const int sel_list = P->mode == 1 ? P->LIST16 : LIST;
-    P->M = 2 * split * sel_list;
-    P->list_len = sel_list;
-  }
+  P->M = 2 * split * P->LIST16;
   P->maxp = (P->M + 63) / 64;
   if (P->maxp > 32) {
     set_error("mepol_knn: refine capacity %d entries per query exceeds 2048", P->M);
@@ -1294,9 +965,7 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   }
   size_t off = 0;
   P->off_apack = off;
-  off = align_up(off + std::max((size_t)P->nct * 64 * P->KSP * sizeof(float),
-                                (size_t)P->nct * 64 * P->KS16 * 16 * sizeof(_Float16)),
-                 256);
+  off = align_up(off + (size_t)P->nct * 64 * P->KS16 * 8 * sizeof(_Float16), 256);
   P->off_scalars = off;  // [0] max |c| bits, [1] fallback count, [2] max |q| bits, [4..5] invalid rows
   off = align_up(off + 32, 256);
   const size_t nl = (size_t)std::max<int64_t>(nq, 1) * P->M;
@@ -1306,72 +975,20 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   off = align_up(off + nl * sizeof(int), 256);
   P->off_flag = off;
   off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(int), 256);
-  P->off_tau = off;
-  off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(float), 256);
-  P->off_cnt = off;
-  off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(int), 256);
+  P->off_part = off;  // exact fallback: kExactGrid partial lists of <= 64 (f64, int32)
+  off = align_up(off + (size_t)kExactGrid * 64 * (sizeof(double) + sizeof(int)), 256);
   P->total = off;
   return 0;
 }
 
-template <int KS>
-static void launch_select_ks(const Plan& P, dim3 g, const float* ap, const float* query, float* lv,
-                             int* li, hipStream_t st) {
-  constexpr int KSP = (KS + 3) / 4 * 4;
-  switch (P.LIST) {
-    case 8:
-      hipLaunchKernelGGL((select_kernel<KS, KSP, 8>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
-                         P.nct, P.split, P.tiles_per_split, lv, li);
-      break;
-    case 16:
-      hipLaunchKernelGGL((select_kernel<KS, KSP, 16>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
-                         P.nct, P.split, P.tiles_per_split, lv, li);
-      break;
-    case 24:
-      hipLaunchKernelGGL((select_kernel<KS, KSP, 24>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
-                         P.nct, P.split, P.tiles_per_split, lv, li);
-      break;
-    case 32:
-      hipLaunchKernelGGL((select_kernel<KS, KSP, 32>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
-                         P.nct, P.split, P.tiles_per_split, lv, li);
-      break;
-    case 40:
-      hipLaunchKernelGGL((select_kernel<KS, KSP, 40>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
-                         P.nct, P.split, P.tiles_per_split, lv, li);
-      break;
-    default:
-      hipLaunchKernelGGL((select_kernel<KS, KSP, 64>), g, dim3(256), 0, st, ap, query, P.nq, P.d,
-                         P.nct, P.split, P.tiles_per_split, lv, li);
-      break;
-  }
-}
-
-// tau_pass: the sampling pass (split 1, every P.sample-th tile) writing tau; otherwise the main
-// selection, seeded by tau when it is non-null.
 template <int KS16>
 static void launch_select16_ks(const Plan& P, const _Float16* ap, const float* query,
-                               const unsigned* scal, float* tau, bool tau_pass, float* lv, int* li,
-                               hipStream_t st) {
-  const unsigned gx = (unsigned)((P.nqt + 3) / 4);
-  if (tau_pass) {
-    const int64_t ns = (P.nct + P.sample - 1) / P.sample;
-#define MEPOL_TAU16(L)                                                                           \
-  hipLaunchKernelGGL((select16_kernel<KS16, L, true>), dim3(gx, 1), dim3(256), 0, st, ap, query, \
-                     P.nq, P.d, ns, 1, ns, P.sample, P.kp1, 0, scal, nullptr, tau, nullptr, nullptr)
-    switch (P.tau_list) {  // >= ceil(kp1 / 2), kp1 <= 60
-      case 8: MEPOL_TAU16(8); break;
-      case 16: MEPOL_TAU16(16); break;
-      case 24: MEPOL_TAU16(24); break;
-      default: MEPOL_TAU16(32); break;
-    }
-#undef MEPOL_TAU16
-    return;
-  }
-#define MEPOL_SEL16(L)                                                                            \
-  hipLaunchKernelGGL((select16_kernel<KS16, L, false>), dim3(gx, (unsigned)P.split), dim3(256), 0, \
-                     st, ap, query, P.nq, P.d, P.nct, P.split, P.tiles_per_split, 1, P.kp1, P.keep, \
-                     scal, tau, nullptr, lv, li)
-  switch (P.LIST16) {  // >= keep + 4 >= 7; mode 1 needs LIST16 <= 40
+                               const unsigned* scal, float* lv, int* li, hipStream_t st) {
+  const dim3 g((unsigned)((P.nqt + 3) / 4), (unsigned)P.split);
+#define MEPOL_SEL16(L)                                                                           \
+  hipLaunchKernelGGL((select16_kernel<KS16, L>), g, dim3(256), 0, st, ap, query, P.nq, P.d,       \
+                     P.nct, P.split, P.tiles_per_split, P.keep, scal, lv, li)
+  switch (P.LIST16) {  // >= keep + 4 >= 7
     case 8: MEPOL_SEL16(8); break;
     case 16: MEPOL_SEL16(16); break;
     case 24: MEPOL_SEL16(24); break;
@@ -1390,55 +1007,59 @@ static int refine_rank_merge() {
   return v;
 }
 
-// KS16 = 4 (d + 1 in 49..64): double-buffered select16 with lists of at most 32, no sampling
-// pass (make_plan)
-static void launch_select16_ks4(const Plan& P, const _Float16* ap, const float* query,
-                                const unsigned* scal, float* tau, float* lv, int* li,
-                                hipStream_t st) {
-  const unsigned gx = (unsigned)((P.nqt + 3) / 4);
-#define MEPOL_SEL16W(L)                                                                          \
-  hipLaunchKernelGGL((select16_kernel<4, L, false>), dim3(gx, (unsigned)P.split), dim3(256), 0, \
-                     st, ap, query, P.nq, P.d, P.nct, P.split, P.tiles_per_split, 1, P.kp1, P.keep, \
-                     scal, tau, nullptr, lv, li)
-  switch (P.LIST16) {
-    case 8: MEPOL_SEL16W(8); break;
-    case 16: MEPOL_SEL16W(16); break;
-    case 24: MEPOL_SEL16W(24); break;
-    default: MEPOL_SEL16W(32); break;
-  }
-#undef MEPOL_SEL16W
-}
-
-template <int LIST>
-static void launch_refine_list(const Plan& P, const float* cand, const float* query,
-                               const float* lv, const int* li, const unsigned* cmax,
-                               const float* tau, const int* counts, double* D, int64_t* I64,
-                               int32_t* I32, int* fc, int* fl, hipStream_t st) {
+static void launch_refine(const Plan& P, const float* cand, const float* query, const float* lv,
+                          const int* li, const unsigned* cmax, double* D, int64_t* I64,
+                          int32_t* I32, int* fc, int* fl, hipStream_t st) {
   dim3 g((unsigned)((P.nq + 3) / 4));
   // MAXP = ceil(M / 64) <= 32
+#define MEPOL_REFINE(MP)                                                                          \
+  hipLaunchKernelGGL((refine_kernel<kRefineList, MP>), g, dim3(256), 0, st, cand, P.nc, query,    \
+                     P.nq, P.d, P.kp1, P.M, P.LIST16, lv, li, cmax, P.e_terms, D, I64, I32, fc,   \
+                     fl, refine_rank_merge())
   if (P.maxp <= 2)
-    hipLaunchKernelGGL((refine_kernel<LIST, 2>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl, refine_rank_merge());
+    MEPOL_REFINE(2);
   else if (P.maxp <= 4)
-    hipLaunchKernelGGL((refine_kernel<LIST, 4>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl, refine_rank_merge());
+    MEPOL_REFINE(4);
   else if (P.maxp <= 8)
-    hipLaunchKernelGGL((refine_kernel<LIST, 8>), g, dim3(256), 0, st, cand, P.nc, query, P.nq, P.d,
-                       P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl, refine_rank_merge());
+    MEPOL_REFINE(8);
   else if (P.maxp <= 16)
-    hipLaunchKernelGGL((refine_kernel<LIST, 16>), g, dim3(256), 0, st, cand, P.nc, query, P.nq,
-                       P.d, P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl, refine_rank_merge());
+    MEPOL_REFINE(16);
   else
-    hipLaunchKernelGGL((refine_kernel<LIST, 32>), g, dim3(256), 0, st, cand, P.nc, query, P.nq,
-                       P.d, P.kp1, P.M, P.list_len, counts, lv, li, cmax, P.e_terms, tau, D, I64, I32, fc, fl, refine_rank_merge());
+    MEPOL_REFINE(32);
+#undef MEPOL_REFINE
 }
 
 template <int LIST>
 static void launch_exact_list(const Plan& P, const float* cand, const float* query, const int* fc,
                               const int* fl, double* D, int64_t* I64, int32_t* I32,
-                              unsigned grid, hipStream_t st) {
+                              unsigned grid, hipStream_t st, double* part_d = nullptr,
+                              int* part_i = nullptr) {
   hipLaunchKernelGGL((exact_kernel<LIST>), dim3(grid), dim3(256), 0, st, cand, P.nc, query, P.nq,
-                     P.d, P.kp1, fc, fl, D, I64, I32);
+                     P.d, P.kp1, fc, fl, D, I64, I32, part_d, part_i);
+  if (part_d)
+    hipLaunchKernelGGL(exact_merge_kernel, dim3(grid), dim3(256), 0, st, (int)grid, P.kp1, P.nq,
+                       fc, fl, part_d, part_i, D, I64, I32);
+}
+
+template <int LIST>
+static void launch_exact(const Plan& P, const float* cand, const float* query, const int* fc,
+                         const int* fl, double* D, int64_t* I64, int32_t* I32, unsigned grid,
+                         hipStream_t st, double* part_d, int* part_i) {
+  launch_exact_list<LIST>(P, cand, query, fc, fl, D, I64, I32, grid, st, part_d, part_i);
+}
+
+static void launch_exact_kp1(const Plan& P, const float* cand, const float* query, const int* fc,
+                             const int* fl, double* D, int64_t* I64, int32_t* I32, unsigned grid,
+                             hipStream_t st, double* part_d, int* part_i) {
+  // per-thread list >= kp1 (kp1 <= 64)
+  if (P.kp1 <= 8)
+    launch_exact<8>(P, cand, query, fc, fl, D, I64, I32, grid, st, part_d, part_i);
+  else if (P.kp1 <= 16)
+    launch_exact<16>(P, cand, query, fc, fl, D, I64, I32, grid, st, part_d, part_i);
+  else if (P.kp1 <= 40)
+    launch_exact<40>(P, cand, query, fc, fl, D, I64, I32, grid, st, part_d, part_i);
+  else
+    launch_exact<64>(P, cand, query, fc, fl, D, I64, I32, grid, st, part_d, part_i);
 }
 
 }  // namespace knn
@@ -1461,8 +1082,8 @@ extern "C" int mepol_knn_plan_info(int64_t n_cand, int64_t n_query, int d, int k
   Plan P;
   int rc = make_plan(n_cand, n_query, d, kp1, split_hint, &P);
   if (rc) return rc;
-  if (ks) *ks = P.KS;
-  if (list) *list = P.LIST;
+  if (ks) *ks = P.KS16;
+  if (list) *list = P.LIST16;
   if (split) *split = P.split;
   return 0;
 }
@@ -1485,18 +1106,17 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
   if (n_query == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  float* apack = (float*)(ws + P.off_apack);
+  _Float16* ap16 = (_Float16*)(ws + P.off_apack);
   unsigned* cmax = (unsigned*)(ws + P.off_scalars);
   int* fcount = n_fallback_out ? (int*)n_fallback_out : (int*)(ws + P.off_scalars + 4);
   float* lv = (float*)(ws + P.off_lv);
   int* li = (int*)(ws + P.off_li);
   int* flist = (int*)(ws + P.off_flag);
-
-  float* tau = nullptr;   // sampled per-query bounds (mode 1 with sampling)
-  int* counts = nullptr;  // survivors per query (filter pass)
+  double* pd = (double*)(ws + P.off_part);
+  int* pi = (int*)(ws + P.off_part + (size_t)kExactGrid * 64 * sizeof(double));
   MEPOL_HIP(hipMemsetAsync(ws + P.off_scalars, 0, 32, st));
   if (n_fallback_out) MEPOL_HIP(hipMemsetAsync(n_fallback_out, 0, sizeof(int32_t), st));
-  // scal[0] = max candidate norm (refine's C), scal[2] = max query norm (split-f16 scale)
+  // scal[0] = max candidate norm (refine's C), scal[2] = max query norm (f16 scale)
   hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nc + 255) / 256)), dim3(256), 0, st, cand,
                      P.nc, P.d, cmax, cmax + 4);
   hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nq + 255) / 256)), dim3(256), 0, st, query,
@@ -1517,81 +1137,26 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
       return kErrUnsupported;
     }
   }
-  if (P.mode == 1) {
-    _Float16* ap16 = (_Float16*)apack;
-    const int64_t total = P.nct * 64;
-    hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
-                       cand, P.nc, P.d, P.KS16, P.nct, ap16, cmax);
-    MEPOL_CHECK_LAUNCH();
-    tau = P.sample ? (float*)(ws + P.off_tau) : nullptr;
-    if (P.filter) {
-      counts = (int*)(ws + P.off_cnt);
-      MEPOL_HIP(hipMemsetAsync(counts, 0, (size_t)P.nq * sizeof(int), st));
-    }
-    for (int pass = tau ? 0 : 1; pass < 2; ++pass) {
-      if (pass == 1 && P.filter) {
-        const dim3 g((unsigned)((P.nqt + 3) / 4), (unsigned)P.split);
-#define MEPOL_FLT16(K)                                                                          \
-  hipLaunchKernelGGL((filter16_kernel<K>), g, dim3(256), 0, st, ap16, query, P.nq, P.d, P.nct,  \
-                     P.split, P.tiles_per_split, cmax, tau, P.M, counts, lv, li)
-        switch (P.KS16) {
-          case 1: MEPOL_FLT16(1); break;
-          case 2: MEPOL_FLT16(2); break;
-          default: MEPOL_FLT16(3); break;
-        }
-#undef MEPOL_FLT16
-        MEPOL_CHECK_LAUNCH();
-        continue;
-      }
-      switch (P.KS16) {  // mode 1 only for KS16 <= 3, or 4 with lists <= 32 (make_plan)
-        case 1: launch_select16_ks<1>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
-        case 2: launch_select16_ks<2>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
-        case 3: launch_select16_ks<3>(P, ap16, query, cmax, tau, pass == 0, lv, li, st); break;
-        default: launch_select16_ks4(P, ap16, query, cmax, tau, lv, li, st); break;
-      }
-      MEPOL_CHECK_LAUNCH();
-    }
-  } else {
-    const int64_t total = P.nct * 64;
-    hipLaunchKernelGGL(pack_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, cand,
-                       P.nc, P.d, P.KSP, P.nct, apack, cmax);
-    MEPOL_CHECK_LAUNCH();
-    dim3 g((unsigned)((P.nqt + 3) / 4), (unsigned)P.split);
-    switch (P.KS) {
-      case 2: launch_select_ks<2>(P, g, apack, query, lv, li, st); break;
-      case 4: launch_select_ks<4>(P, g, apack, query, lv, li, st); break;
-      case 8: launch_select_ks<8>(P, g, apack, query, lv, li, st); break;
-      case 12: launch_select_ks<12>(P, g, apack, query, lv, li, st); break;
-      case 15: launch_select_ks<15>(P, g, apack, query, lv, li, st); break;
-      case 16: launch_select_ks<16>(P, g, apack, query, lv, li, st); break;
-      case 24: launch_select_ks<24>(P, g, apack, query, lv, li, st); break;
-      default: launch_select_ks<32>(P, g, apack, query, lv, li, st); break;
-    }
-    MEPOL_CHECK_LAUNCH();
-  }
-  switch (P.LIST) {
-    case 8: launch_refine_list<8>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
-    case 16: launch_refine_list<16>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
-    case 24: launch_refine_list<24>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
-    case 32: launch_refine_list<32>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
-    case 40: launch_refine_list<40>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
-    default: launch_refine_list<64>(P, cand, query, lv, li, cmax, tau, counts, dist_out, idx_out, idx32_out, fcount, flist, st); break;
+  const int64_t total = P.nct * 64;
+  hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, cand,
+                     P.nc, P.d, P.KS16, P.nct, ap16, cmax);
+  MEPOL_CHECK_LAUNCH();
+  switch (P.KS16) {
+    case 1: launch_select16_ks<1>(P, ap16, query, cmax, lv, li, st); break;
+    case 2: launch_select16_ks<2>(P, ap16, query, cmax, lv, li, st); break;
+    case 3: launch_select16_ks<3>(P, ap16, query, cmax, lv, li, st); break;
+    default: launch_select16_ks<4>(P, ap16, query, cmax, lv, li, st); break;
   }
   MEPOL_CHECK_LAUNCH();
-  const unsigned eg = 512;
-  switch (P.LIST) {
-    case 8: launch_exact_list<8>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
-    case 16: launch_exact_list<16>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
-    case 24: launch_exact_list<24>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
-    case 32: launch_exact_list<32>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
-    case 40: launch_exact_list<40>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
-    default: launch_exact_list<64>(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, eg, st); break;
-  }
+  launch_refine(P, cand, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st);
+  MEPOL_CHECK_LAUNCH();
+  launch_exact_kp1(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, kExactGrid, st,
+                   pd, pi);
   MEPOL_CHECK_LAUNCH();
   return 0;
 }
 
-// Exhaustive exact k-NN for every query (no fp32 selection): the reference semantics at the
+// Exhaustive exact k-NN for every query (no f16 selection): the reference semantics at the
 // cost of a full f64 scan.  Used for d > 63 / k+1 > 60 and as an independent check.
 extern "C" int mepol_knn_exact(const float* cand, int64_t n_cand, const float* query,
                                int64_t n_query, int d, int kp1, double* dist_out, int64_t* idx_out,

@@ -77,7 +77,7 @@ def knn_plan(n_cand, n_query, d, kp1, split=0):
     ks, lst, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     call("mepol_knn_plan_info", n_cand, n_query, d, kp1, split, ctypes.byref(ks),
          ctypes.byref(lst), ctypes.byref(sp))
-    return {"KS": ks.value, "LIST": lst.value, "split": sp.value}
+    return {"KS16": ks.value, "LIST16": lst.value, "split": sp.value}
 
 
 def knn(cand, kp1, query=None, split=0, want_int64=True, return_fallback=False):
@@ -132,7 +132,7 @@ def knn_exact(cand, kp1, query=None, want_int64=True):
     return D, I, I32T
 
 
-def iw_forward(logp_t, logp_b, offsets, n_particles, normalize=True, w_out=None):
+def iw_forward(logp_t, logp_b, offsets, n_particles, normalize=True, w_out=None, u_out=None):
     """u = exp(segmented cumsum(logp_t - logp_b)); w = u / sum(u).
 
     logp_t/logp_b: f64 [nt, T_stride]; offsets: int64 [nt+1] particle offsets.
@@ -143,7 +143,7 @@ def iw_forward(logp_t, logp_b, offsets, n_particles, normalize=True, w_out=None)
     dev = logp_t.device
     lt = logp_t.contiguous()
     lb = logp_b.contiguous()
-    u = torch.empty(n_particles, dtype=torch.float64, device=dev)
+    u = u_out if u_out is not None else torch.empty(n_particles, dtype=torch.float64, device=dev)
     ts = torch.empty(nt, dtype=torch.float64, device=dev)
     w = (w_out if w_out is not None else torch.empty(n_particles, dtype=torch.float64,
                                                      device=dev)) if normalize else None
@@ -153,8 +153,8 @@ def iw_forward(logp_t, logp_b, offsets, n_particles, normalize=True, w_out=None)
     return u, ts, w, U
 
 
-def iw_normalize(u, U):
-    w = torch.empty_like(u)
+def iw_normalize(u, U, out=None):
+    w = out if out is not None else torch.empty_like(u)
     call("mepol_iw_normalize", ptr(u), ptr(U), u.numel(), ptr(w), _stream())
     return w
 
@@ -405,10 +405,19 @@ def rollout_mlp(env_id, W1, b1, W2, b2, Wm, bm, log_std, init, noise, states_rec
     W2t = W2.t().contiguous()
     init64 = init.contiguous() if env_id == 0 else None
     init32 = init.contiguous() if env_id == 1 else None
+    import ctypes
+
+    nbytes = ctypes.c_size_t()
+    call("mepol_rollout_mlp_workspace_size", n, h0, h1, ctypes.byref(nbytes))
+    ws = _workspace(init.device, nbytes.value, tag="rollout")
     call("mepol_rollout_mlp", env_id, ptr(W1.contiguous()), ptr(b1), h0, ptr(W2t), ptr(b2), h1,
          ptr(Wm.contiguous()), ptr(bm), ptr(log_std.contiguous()), a_dim, ptr(init64), ptr(init32),
          ptr(noise.contiguous()), n, T, ptr(states_rec), ptr(actions_rec), ptr(visited), None,
-         _stream())
+         ptr(ws), ws.numel(), _stream())
+    # word 0: the multi-workgroup form's flag (its workgroups could not all run at once)
+    if int(ws[:4].view(torch.int32)[0].item()) != 0:
+        raise _lib.MepolError("mepol_rollout_mlp: the workgroups of a trajectory were not co-resident "
+                         "(MEPOL_ROLLOUT_MW=0 selects the one-workgroup form)")
 
 
 def memcpy_async(dst, src):

@@ -102,6 +102,14 @@ class ShardedEpoch:
                 self._logp_b = (key, self._logp(policy).detach())
         return self._logp_b[1]
 
+    def seed_behavioral_logp(self, policy, logp):
+        """Cache `logp` (computed at the policy's current parameters) as its behavioral
+        log-probabilities (ParticleBatch.seed_behavioral_logp)."""
+        from .algorithms.particles import _param_key
+
+        with torch.no_grad():
+            self._logp_b = (_param_key(policy), logp.detach().reshape(self.nt, self.T).clone())
+
     def _logps(self, beh, tgt):
         from .algorithms.particles import _param_key
 
@@ -215,6 +223,10 @@ class ShardedEpoch:
             def make_device_loop(opt, b, t):
                 return self.device_loop(opt, b, t, G, B, ns, eps)
 
+            @staticmethod
+            def seed_behavioral_logp(policy, logp):
+                self.seed_behavioral_logp(policy, logp)
+
         return off_policy_optimization(optimizer, beh, tgt, last_valid, None, None, self.nt, None,
                                        None, None, k, G, B, ns, eps, kl_threshold, max_off_iters,
                                        use_backtracking, backtrack_coeff, max_backtrack_try,
@@ -238,12 +250,20 @@ class ShardedEpoch:
             _SHARDED_CACHE.pop(tgt, None)
             it = ShardedIteration(tgt, optimizer, self, G, B, ns, eps)
             _SHARDED_CACHE[tgt] = it
-        it.attach(self, self.behavioral_logp(beh))
+        from .algorithms.mepol import _same_params
+
+        # At an epoch's start the target holds the behavioral parameters (mepol.py:409, 493):
+        # one forward into the loop's buffers is logp_b and the first replay's activations.
+        same = _same_params(tgt, beh)
+        it.attach(self, None if same else self.behavioral_logp(beh))
+        if same:
+            self.seed_behavioral_logp(beh, it.start_from_behavioral())
         if it.graph is None and not it.try_capture():
             _GRAPH_STATE["disabled"] = True
             _SHARDED_CACHE.pop(tgt, None)
             return None
-        it.refresh()
+        if not same:
+            it.refresh()
         return it
 
 
@@ -273,53 +293,89 @@ _GRAPH_STATE = {}
 
 
 class ShardedIteration(DeviceIteration):
-    """policy_update + compute_kl of a ShardedEpoch as one graph, with the RCCL all-gathers
-    and the gradient all-reduce of the eager path (same algebra, same order) captured."""
+    """policy_update + compute_kl of a ShardedEpoch as one graph with the one-rank iteration's
+    single-pass structure: the forward at theta_t+1 yields KL(theta_t+1) and the next replay's
+    H(theta_t+1) and dH/dW, kept in static buffers (``_prime`` fills them before the first replay
+    and after a rejected step).  Collectives per replay (every rank issues the same sequence):
+
+      1. all-gather of one f64: the per-rank partial of S = sum_j gamma_j w_j   (8 B per rank)
+      2. all-reduce of the flattened policy gradients                       (~1.1 MB at C3)
+      3. all-gather of [u (n_local), sum u]: unnormalised weights + normaliser (n_local + 1 f64)
+      4. all-gather of [dH/dW (n_local), H-sum, KL-sum]                        (n_local + 2 f64)
+
+    Reductions over ranks are fixed-order sums of gathered values, so every rank holds the same
+    bits and takes the same accept/backtrack branch (mepol.py:441-476)."""
 
     def __init__(self, tgt, optimizer, ep, G, B, ns, eps):
         super().__init__(tgt, optimizer, _LocalView(ep), ep.k, G, B, ns, eps)
         self.dist, self.group, self.world = ep.dist, ep.group, ep.world
         self.N_global = ep.N
+        self.R0 = ep.R0
         self.ep = ep
+        f64 = dict(dtype=torch.float64, device=self.device)
+        n, W = self.N, self.world
+        self.xs = torch.zeros(1, **f64)
+        self.xs_all = torch.zeros(W, **f64)
+        self.xu = torch.zeros(n + 1, **f64)
+        self.xu_all = torch.zeros(W * (n + 1), **f64)
+        self.xg = torch.zeros(n + 2, **f64)
+        self.xg_all = torch.zeros(W * (n + 2), **f64)
+        self.u_glob = torch.zeros(self.N_global, **f64)
+        self.w_glob = torch.zeros(self.N_global, **f64)   # importance weights at theta_t
+        self.g_glob = torch.zeros(self.N_global, **f64)   # dH/dW at theta_t, every particle
+        self.sums_cur = torch.zeros(2, **f64)             # [H-sum, KL-sum] at theta_t
 
     def matches_epoch(self, tgt, optimizer, ep, G, B, ns, eps):
         return (self.matches(tgt, optimizer, _LocalView(ep), ep.k, G, B, ns, eps)
-                and ep.N == self.N_global and ep.world == self.world
+                and ep.N == self.N_global and ep.world == self.world and ep.R0 == self.R0
                 and ep.dist is self.dist and ep.group is self.group)
 
-    # the sharded body computes its weights from logp each replay (collectives), so a refresh
-    # is the forward alone
-    def refresh(self):
-        self.forward()
-
-    def attach(self, ep, logp_b):
+    def attach(self, ep, logp_b=None):
         self.ep = ep
         self.load(_LocalView(ep), logp_b)
 
-    def _weights(self, lt):
-        ep, ops = self.ep, self.ep.ops
-        u, ts, _, _ = ops.iw_forward(lt, self.logp_b, self.offsets, self.N, normalize=False)
-        U = ep._sum(ts.sum().reshape(1)).reshape(())
-        w_local = ops.iw_normalize(u, U)
-        return w_local, ep._gather(w_local).reshape(self.N_global)
+    def _gather_into(self, out, t):
+        self.dist.all_gather_into_tensor(out, t, group=self.group)
+
+    def _fwd_exchange(self):
+        """Weights, dH/dW and the [H-sum, KL-sum] of self.logp (the last forward) over all
+        ranks: collectives 3 and 4.  w_glob / g_glob are overwritten."""
+        ops, n, W = self.ep.ops, self.N, self.world
+        lt = self.logp.view(self.nt, self.T)
+        _, ts, _, _ = ops.iw_forward(lt, self.logp_b, self.offsets, n, normalize=False,
+                                     u_out=self.xu[:n])
+        torch.sum(ts, 0, keepdim=True, out=self.xu[n:])
+        self._gather_into(self.xu_all, self.xu)
+        xa = self.xu_all.view(W, n + 1)
+        U = xa[:, n].sum()                        # fixed-order sum of the per-rank normalisers
+        self.u_glob.view(W, n).copy_(xa[:, :n])
+        ops.iw_normalize(self.u_glob, U, out=self.w_glob)
+        out4, _, _ = ops.entropy_forward(self.w_glob, self.idx32T, self.D, self.k, self.ns,
+                                         self.G, self.B, self.eps, n_w=self.N_global,
+                                         g_out=self.xg[:n])
+        self.xg[n:].copy_(out4[2:4])
+        self._gather_into(self.xg_all, self.xg)
+        xg = self.xg_all.view(W, n + 2)
+        self.g_glob.view(W, n).copy_(xg[:, :n])
+        return xg[:, n:].sum(0)
+
+    @torch.no_grad()
+    def _prime(self):
+        self.sums_cur.copy_(self._fwd_exchange())
 
     @torch.no_grad()
     def _body(self):
         self._scal_in()
-        ep, ops = self.ep, self.ep.ops
-        W1, b1, W2, b2, Wm, bm, ls = self.named
-        nt, T, k = self.nt, self.T, self.k
-        lt = self.logp.view(nt, T)
-        # H at theta_t (ShardedEpoch.weights / entropy_sums)
-        w_local, w_global = self._weights(lt)
-        out4, _, g = ops.entropy_forward(w_global, self.idx32T, self.D, k, self.ns, self.G,
-                                         self.B, self.eps, n_w=self.N_global)
-        sums_h = ep._sum(out4[2:4].contiguous())
-        # dH/dlogp (_ShardedEntropy.backward)
-        g_global = ep._gather(g).reshape(self.N_global)
-        gamma, partials, nparts = ops.entropy_gamma(g_global, w_local, self.csr_off,
+        ops = self.ep.ops
+        nt, T, n = self.nt, self.T, self.N
+        # dH/dlogp at theta_t (_ShardedEntropy.backward) from the weights / dH/dW the previous
+        # replay (or _prime) left
+        w_local = self.w_glob[self.R0:self.R0 + n]
+        gamma, partials, nparts = ops.entropy_gamma(self.g_glob, w_local, self.csr_off,
                                                     self.csr_rows)
-        S = ep._sum(partials[:nparts].sum().reshape(1)).reshape(())
+        torch.sum(partials[:nparts], 0, keepdim=True, out=self.xs)
+        self._gather_into(self.xs_all, self.xs)
+        S = self.xs_all.sum()
         grad = ops.entropy_reverse_scan(gamma, w_local, partials, nparts, self.offsets, nt, T,
                                         self.neg_one, S_ext=S)
         dW1, db1, dW2, db2, dWm, dbm, dls = self._backward(grad.view(-1))
@@ -331,15 +387,11 @@ class ShardedIteration(DeviceIteration):
             grads.append(flat[o:o + p.numel()].view_as(p))
             o += p.numel()
         self._optim_step(grads)
-        # KL at theta_t+1 (ShardedEpoch.compute_kl)
+        # KL at theta_t+1 (ShardedEpoch.compute_kl); H(theta_t+1) and dH/dW for the next replay
         self.forward()
-        _, w2 = self._weights(lt)
-        out4k, _, _ = ops.entropy_forward(w2, self.idx32T, self.D, k, 1.0, 1.0, 0.0,
-                                          self.eps, n_w=self.N_global)
-        sums_k = ep._sum(out4k[2:4].contiguous())
-        H = -sums_h[0] + self.B
-        KL = sums_k[1] / self.N_global
-        torch.stack((H, KL), out=self.vals)
+        sums = self._fwd_exchange()
+        torch.stack((self.B - self.sums_cur[0], sums[1] / self.N_global), out=self.vals)
+        self.sums_cur.copy_(sums)
         self._vals_out()
 
     def try_capture(self):

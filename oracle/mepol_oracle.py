@@ -10,7 +10,10 @@ log-probs recomputed every call) so that it also serves as the CPU wall-clock ba
 Pinned against the golden fixtures in tests/golden/ produced by running the reference itself
 (tests/golden/make_golden.py); see tests/test_oracle_golden.py.
 """
+import ctypes
 import math
+import os
+import subprocess
 
 import numpy as np
 import torch
@@ -222,6 +225,55 @@ def rollout(env, sd, log_std, init, noise, T):
         actions[:, t] = a
         s = mountaincar_step(s, a) if env == "mountaincar" else gridworld_step(s, a)
         states[:, t + 1] = s
+    return states, actions
+
+
+_NATIVE = {}
+
+
+def _native():
+    """oracle/native/librollout_kordered.so (gcc; `make` builds it, else built here)."""
+    if "lib" not in _NATIVE:
+        here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+        src = os.path.join(here, "rollout_kordered.c")
+        so = os.path.join(here, "librollout_kordered.so")
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-fPIC", "-shared", src, "-o", so,
+                            "-lm"], check=True)
+        lib = ctypes.CDLL(so)
+        vp, i64, ci = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
+        lib.rollout_kordered.argtypes = [ci, i64, i64, ci, ci, ci] + [vp] * 12
+        lib.rollout_kordered.restype = ci
+        _NATIVE["lib"] = lib
+    return _NATIVE["lib"]
+
+
+def rollout_kordered(env, sd, std, init, noise, T):
+    """collect_particles (mepol.py:76-109) for the 2 -> [h0, h1] -> a ReLU policy with the MLP
+    summed in the documented k-ordered / butterfly order of oracle/native/rollout_kordered.c
+    (the order the HIP rollout kernels commit to), so actions compare bit for bit.
+    std: exp(log_std) [a] f64; init [nt, 2] (f64 MountainCar, f32 GridWorld); noise [T, nt, a].
+    Returns states f32 [nt, T+1, 2], actions f32 [nt, T, a]."""
+    def arr(x, dt):
+        return np.ascontiguousarray(np.asarray(x, dtype=dt))
+
+    W1, b1 = arr(sd["net.0.weight"], np.float64), arr(sd["net.0.bias"], np.float64)
+    W2, b2 = arr(sd["net.2.weight"], np.float64), arr(sd["net.2.bias"], np.float64)
+    Wm, bm = arr(sd["mean.weight"], np.float64), arr(sd["mean.bias"], np.float64)
+    h0, h1, a_dim = W1.shape[0], W2.shape[0], Wm.shape[0]
+    nt = init.shape[0]
+    mc = env == "mountaincar"
+    i64 = arr(init, np.float64) if mc else None
+    i32 = None if mc else arr(init, np.float32)
+    nz = arr(noise, np.float64)
+    sdv = arr(std, np.float64)
+    states = np.zeros((nt, T + 1, 2), np.float32)
+    actions = np.zeros((nt, T, a_dim), np.float32)
+    p = lambda x: None if x is None else x.ctypes.data  # noqa: E731
+    rc = _native().rollout_kordered(0 if mc else 1, nt, T, h0, h1, a_dim, p(W1), p(b1), p(W2),
+                                    p(b2), p(Wm), p(bm), p(sdv), p(i64), p(i32), p(nz),
+                                    p(states), p(actions))
+    assert rc == 0
     return states, actions
 
 

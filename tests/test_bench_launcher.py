@@ -31,8 +31,34 @@ def test_bench_workloads_parse():
     sys.path.insert(0, ROOT)
     import bench
 
-    for w in ("C2", "C2S", "C3", "C4", "C5"):
+    for w in ("C2", "C2S", "C3", "C4", "C5", "C3R8", "C4R8", "C5R8"):
         cfg = bench.WORKLOADS[w]
         assert cfg["num_traj"] % 8 == 0 or w.startswith("C2")
         args = bench.parse(["--workload", w, "--gpus", "2"])
         assert args.workload == w and args.gpus == 2
+
+
+def test_emulated_dist_fills_peer_slots():
+    """The R8 workloads run rank 0 of an 8-rank job on one GPU: every collective becomes local
+    copies of the same size; gathers take registered peer tensors (the other shards' next states,
+    so the k-NN sees all N candidates) or replicate rank 0's payload."""
+    import torch
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    d = bench._EmulatedDist(4)
+    assert d.get_world_size() == 4 and d.get_rank() == 0 and d.get_backend() == "nccl"
+    own = torch.arange(6, dtype=torch.float32).reshape(3, 2)
+    d.peers = [torch.full((3, 2), float(r)) for r in (1, 2, 3)]
+    out = torch.empty(4 * 6, dtype=torch.float32)
+    d.all_gather_into_tensor(out, own)
+    o = out.view(4, 3, 2)
+    assert torch.equal(o[0], own) and all(bool((o[r] == r).all()) for r in (1, 2, 3))
+    w = torch.arange(5, dtype=torch.float64)
+    outw = torch.empty(20, dtype=torch.float64)
+    d.all_gather_into_tensor(outw, w)            # no peer of this shape: rank 0's payload
+    assert torch.equal(outw.view(4, 5), w.expand(4, 5))
+    g = torch.ones(3, dtype=torch.float64)
+    d.all_reduce(g)
+    assert torch.equal(g, torch.ones(3, dtype=torch.float64))

@@ -179,3 +179,50 @@ def test_rollout_mlp_kernel_matches_oracle(cuda, monkeypatch, env, kr):
     assert (S == S_ref).mean() > 0.99
     assert np.abs(S - S_ref).max() < 1e-3
     assert np.array_equal(visited.cpu().numpy().astype(np.float32), S[:, 1:])
+
+
+@pytest.mark.parametrize("env", ["mountaincar", "gridworld"])
+@pytest.mark.parametrize("mw", ["1", "0"], ids=["multi-wg", "one-wg"])
+@pytest.mark.parametrize("hidden", [[300, 300], [64, 48], [400, 300]])
+def test_rollout_mlp_bitexact_vs_kordered_oracle(cuda, monkeypatch, env, mw, hidden):
+    """mepol_rollout_mlp against the oracle's k-ordered restatement
+    (oracle/native/rollout_kordered.c: the MLP summed in the order the kernels commit to): the
+    actions are bit-identical and so are the GridWorld states (f32 state, f64 move: no
+    transcendental); MountainCar's cos() may round differently from glibc in the last ulp, so
+    its states / actions are checked to 1e-12.  Both kernel forms (ceil(h1/64) workgroups per
+    trajectory, MEPOL_ROLLOUT_MW=1, and one workgroup per trajectory) give the same bits."""
+    from mepol_amd import ops
+    from mepol_amd.policy import GaussianPolicy
+
+    monkeypatch.setenv("MEPOL_ROLLOUT_MW", mw)
+    torch.manual_seed(11)
+    a_dim = 1 if env == "mountaincar" else 2
+    pol = GaussianPolicy(hidden, 2, a_dim, -0.5 if env == "mountaincar" else -1.5).cuda()
+    nt, T = 20, 60
+    rng = np.random.default_rng(3)
+    if env == "mountaincar":
+        init = np.stack([rng.uniform(-0.6, -0.4, nt), np.zeros(nt)], 1)
+    else:
+        init = rng.uniform(-6, -4, (nt, 2)).astype(np.float32)
+    noise = rng.standard_normal((T, nt, a_dim))
+    sd = {k: v.detach().cpu().numpy() for k, v in pol.state_dict().items()}
+    # exp(log_std) as the device computes it (ocml); it agrees with numpy's to an ulp
+    std_dev = torch.exp(pol.log_std.detach()).cpu().numpy()
+    np.testing.assert_allclose(std_dev, np.exp(sd["log_std"]), rtol=2.3e-16, atol=0)
+    S_ref, A_ref = O.rollout_kordered(env, sd, std_dev, init, noise, T)
+    dev = "cuda"
+    states = torch.zeros((nt, T + 1, 2), dtype=torch.float32, device=dev)
+    actions = torch.zeros((nt, T, a_dim), dtype=torch.float32, device=dev)
+    l1, l2 = pol.net[0], pol.net[2]
+    ops.rollout_mlp(0 if env == "mountaincar" else 1, l1.weight.detach(), l1.bias.detach(),
+                    l2.weight.detach(), l2.bias.detach(), pol.mean.weight.detach(),
+                    pol.mean.bias.detach(), pol.log_std.detach(), torch.as_tensor(init, device=dev),
+                    torch.as_tensor(noise, dtype=torch.float64, device=dev), states, actions)
+    S, A = states.cpu().numpy(), actions.cpu().numpy()
+    if env == "gridworld":
+        assert np.array_equal(A, A_ref)
+        assert np.array_equal(S, S_ref)
+    else:
+        assert np.array_equal(A[:, 0], A_ref[:, 0])  # first step: no cos() involved yet
+        np.testing.assert_allclose(A, A_ref, rtol=0, atol=1e-12)
+        np.testing.assert_allclose(S, S_ref, rtol=0, atol=1e-12)

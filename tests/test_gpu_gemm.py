@@ -1,5 +1,4 @@
 """f64 GEMM kernels (csrc/gemm.hip): the MFMA tilings and the DPP-VALU experiment == torch f64."""
-import ctypes
 
 import pytest
 import torch
@@ -23,21 +22,6 @@ def test_gemm_nt_matches_torch(cuda, n, k, m, variant):
     torch.testing.assert_close(out, ref, rtol=1e-12, atol=1e-12)
     torch.testing.assert_close(ops.gemm_nt(A, B, variant=variant), A @ B.t(), rtol=1e-12,
                                atol=1e-12)
-
-
-@pytest.mark.parametrize("n,k,m", SHAPES)
-@pytest.mark.parametrize("variant", [0, 5, 8])
-def test_gemm_dpp_matches_torch(cuda, n, k, m, variant):
-    from mepol_amd import _lib
-
-    torch.manual_seed(n * 7 + k + m)
-    A = torch.randn(n, k, dtype=torch.float64, device="cuda")
-    B = torch.randn(m, k, dtype=torch.float64, device="cuda")
-    C = torch.empty(n, m, dtype=torch.float64, device="cuda")
-    _lib.call("mepol_gemm_dpp", _lib.ptr(A), n, k, A.stride(0), _lib.ptr(B), m, B.stride(0),
-              None, 0, _lib.ptr(C), C.stride(0), variant,
-              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-    torch.testing.assert_close(C, A @ B.t(), rtol=1e-12, atol=1e-12)
 
 
 def test_gemm_nt_rejects_odd_k(cuda):

@@ -151,17 +151,34 @@ def test_knn_rejects_non_finite(cuda, bad, where):
     assert np.array_equal(D.cpu().numpy(), Do) and np.array_equal(I.cpu().numpy(), Io)
 
 
-@pytest.mark.parametrize("env", [{"MEPOL_KNN_SAMPLE": "8"}, {"MEPOL_KNN_SAMPLE": "8", "MEPOL_KNN_FILTER": "0"},
-                                 {"MEPOL_KNN_PRECISION": "f32"}, {"MEPOL_KNN_SAMPLE": "4", "MEPOL_KNN_CAP": "256"}])
-def test_knn_optional_paths_bitexact(cuda, monkeypatch, env):
-    """The tuning switches (sampled bound + survivor filter, sampled bound + lists, the f32 MFMA
-    selection, a small survivor cap that sends queries to the exhaustive path) change only the
-    candidate screening: the certified f64 output stays bit-identical to the default path."""
-    rng = np.random.default_rng(11)
-    X = rng.standard_normal((40000, 29)).astype(np.float32)
-    D0, I0, _, _ = _knn(X, 31)
-    for key, val in env.items():
-        monkeypatch.setenv(key, val)
-    D1, I1, _, _ = _knn(X, 31)
-    assert np.array_equal(D0, D1)
-    assert np.array_equal(I0, I1)
+def test_knn_fallback_heavy_input_matches_oracle(cuda):
+    """Many uncertified queries (heavy duplicate clusters with near-ties): the chunked
+    exhaustive path (exact_kernel over the whole grid + exact_merge_kernel) answers them, and the
+    result is still bit-exact against the oracle."""
+    rng = np.random.default_rng(5)
+    base = rng.standard_normal((40, 12)).astype(np.float32)
+    X = np.repeat(base, 60, axis=0)                      # 2400 rows, 40 clusters of 60 copies
+    X[::7] += np.float32(1e-6) * rng.standard_normal((len(X[::7]), 12)).astype(np.float32)
+    for kp1 in (5, 31, 60):
+        D, I, _, nfb = _knn(X, kp1)
+        Do, Io = O.knn_exact(X, kp1)
+        assert nfb > 0
+        assert np.array_equal(D, Do) and np.array_equal(I, Io)
+
+
+@pytest.mark.parametrize("nq", [1, 3, 40])
+def test_knn_exact_chunked_few_queries(cuda, nq):
+    """Few queued queries spread over the grid (count < 512 blocks: chunked scan + merge):
+    bit-exact against the oracle for a query subset with duplicated candidates."""
+    from mepol_amd import ops
+
+    rng = np.random.default_rng(nq)
+    X = rng.standard_normal((20000, 7)).astype(np.float32)
+    X[5000:5100] = X[0]                                   # a cluster of 101 identical rows
+    Q = np.concatenate([X[:nq // 2 + 1], rng.standard_normal((nq - nq // 2 - 1, 7))]).astype(
+        np.float32)[:nq]
+    Xt = torch.as_tensor(X, device="cuda")
+    D, I, _, nfb = ops.knn(Xt, 51, query=torch.as_tensor(Q, device="cuda"), return_fallback=True)
+    Do, Io = O.knn_exact(X, 51, Q=Q)
+    assert np.array_equal(D.cpu().numpy(), Do) and np.array_equal(I.cpu().numpy(), Io)
+

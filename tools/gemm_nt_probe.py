@@ -32,7 +32,9 @@ if KIND == "dpp":
 
     from mepol_amd import _lib
 
-    _fn = _lib.load().mepol_gemm_dpp
+    # the DPP GEMM experiment lives outside the product library (tools/variants/build_dpp.sh)
+    _fn = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "variants",
+                                   "libdpp_gemm.so")).mepol_gemm_dpp
     _fn.argtypes = _lib.SIGNATURES["mepol_gemm_nt"]
 
     def _dpp(A, B, bias, relu=False, out=None, variant=0):

@@ -19,6 +19,15 @@ for step in "$@"; do
       (cd /tmp && export TMPDIR=/tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats \
         --output-format csv -d $out/prof_$tag -o run -- \
         python $root/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $out/profbench_$tag.log 2>&1) ;;
+    clk)
+      # effective clock of the f64 MFMA kernels and of the pure-MFMA probe (GRBM_GUI_ACTIVE is
+      # summed over the 8 XCDs; MI355X_MICROARCH.md HBM/rocprofv3 section)
+      for t in mlp:"python $root/tools/mlp_kernels_once.py" probe:"$root/tools/f64_rate_probe"; do
+        name=${t%%:*}; cmd=${t#*:}
+        (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE \
+          SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_F64 SQ_WAVE_CYCLES \
+          --output-format csv -d $out/clk_$name -o run -- $cmd > $out/clk_$name.log 2>&1)
+      done ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $c -d $out/pmc_$c -o run -- \

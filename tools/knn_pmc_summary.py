@@ -3,7 +3,7 @@
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  Per MI355X_MICROARCH.md (HBM section) FETCH_SIZE
 is doubled on gfx950 (it tallies 128-B requests at 64 B); WRITE_SIZE is taken as reported.
 The k-NN call is pack + select + refine (+ exact fallback); the last call of the run is used.
-Writes profiles/knn_pmc.json (read by bench.py for roofline.traffic).
+Writes profiles/knn_pmc_C3.json (read by bench.py for roofline.traffic).
 """
 import json
 import os
@@ -39,7 +39,7 @@ def main(src="gpurun_out"):
     out = {"hbm_bytes_per_launch": total, "kernels": kernels,
            "workload": "C3 k-NN: N=200000 queries x 200000 candidates, d=29, k+1=31",
            "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KiB -> bytes"}
-    path = os.path.join(ROOT, "profiles", "knn_pmc.json")
+    path = os.path.join(ROOT, "profiles", "knn_pmc_C3.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1))
 

@@ -27,10 +27,16 @@ C = torch.empty(N, H1, **f64)
 side = torch.cuda.Stream()
 
 
+# the DPP GEMM experiment lives outside the product library (tools/variants/build_dpp.sh)
+_DPP = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "variants",
+                                "libdpp_gemm.so")).mepol_gemm_dpp
+_DPP.argtypes = _lib.SIGNATURES["mepol_gemm_nt"]
+
+
 def dpp(variant):
     def run():
-        _lib.call("mepol_gemm_dpp", _lib.ptr(A), N, H0, H0, _lib.ptr(B), H1, H0, None, 0,
-                  _lib.ptr(C), H1, variant, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        assert _DPP(_lib.ptr(A), N, H0, H0, _lib.ptr(B), H1, H0, None, 0, _lib.ptr(C), H1,
+                    variant, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
     return run
 
 
