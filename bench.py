@@ -391,13 +391,18 @@ def run(args):
     nq = N // shards
     F = 3.0 * d * nq * N                      # algorithmic flops
     knn_tflops = F / (knn_ms * 1e-3) / 1e12
-    # The selection (csrc/knn.hip): candidate-hi f16 MFMA, 2 products (q_hi, q_lo) x 2 x K flops
-    # per (query, candidate), K = 16*ceil((d+1)/16), f32 accumulate; then the f64 refine.
-    K16 = 16 * ((d + 1 + 15) // 16)
-    knn_issued = 2 * 2 * K16 * float(nq) * N
+    # The selection (csrc/knn.hip, make_plan): f16 MFMA with the candidates' hi half (nh = 1,
+    # 2 products: q_hi, q_lo) or hi + lo halves (nh = 2, 3 products), 2 x K flops each per
+    # (query, candidate), K = 16*ceil((d+1)/16), f32 accumulate; then the certified f64 refine.
+    from mepol_amd import ops as _ops
+
+    plan = _ops.knn_plan(N, nq, d, k + 1)
+    K16 = 16 * plan["KS16"]
+    knn_issued = (1 + plan["nh"]) * 2 * K16 * float(nq) * N
     knn_peak = PEAK_F16_TFLOPS
-    knn_desc = ("f16 MFMA selection (candidate hi half x split query, f32 accumulate) + "
-                "certified f64 exact refine (bit-exact output)")
+    knn_desc = (("f16 MFMA selection (candidate hi half x split query" if plan["nh"] == 1 else
+                 "f16 MFMA selection (split candidate x split query, 3 products")
+                + ", f32 accumulate) + certified f64 exact refine (bit-exact output)")
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", f"knn_pmc_{args.workload}.json")
     if args.workload == "C3" and not os.path.exists(pmc_path):

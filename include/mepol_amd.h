@@ -39,6 +39,19 @@ const char* mepol_last_error_string(void);
 int mepol_abi_version(void);
 /* Stream-ordered copy (device <-> pinned host / device); captured as a graph memcpy node. */
 int mepol_memcpy_async(void* dst, const void* src, size_t bytes, void* stream);
+/* Pinned host memory mapped into the device address space (hipHostMallocMapped): the host
+ * reads / writes it at *host_ptr, kernels at *dev_ptr.  Used for the per-replay scalars of the
+ * captured off-policy iteration (no memcpy nodes in the graph). */
+int mepol_host_alloc_mapped(size_t bytes, void** host_ptr, void** dev_ptr);
+int mepol_host_free(void* host_ptr);
+/* dst[0..n) = src[0..n), n <= 64 f64, one wave; to_host = 0: src is mapped host memory
+ * (mepol_host_alloc_mapped), 1: dst is.  The mapped side is accessed at system scope. */
+int mepol_small_copy(double* dst, const double* src, int n, int to_host, void* stream);
+/* vals[0] = a[ia], vals[1] = b[ib] (both read first), then cur[0..n) = nw[0..n), n <= 64:
+ * the iteration's control outputs (H(theta_t), KL(theta_t+1)) to mapped host memory and the
+ * next replay's entropy sums, in one launch (mepol.py:429-439 reads these two scalars). */
+int mepol_scalars_emit(const double* a, int ia, const double* b, int ib, double* vals,
+                       double* cur, const double* nw, int n, void* stream);
 
 /* ---- k-NN ---------------------------------------------------------------------------------
  * Replaces src/algorithms/mepol.py:190-192
@@ -56,6 +69,8 @@ int mepol_memcpy_async(void* dst, const void* src, size_t bytes, void* stream);
  * (before the scan is launched), as the reference's kneighbors call blocks. */
 int mepol_knn_workspace_size(int64_t n_cand, int64_t n_query, int d, int kp1, int split_hint,
                              size_t* bytes);
+/* Plan of a call: *ks = 10 * (k-steps of 16) + candidate halves (1: f16 hi only, 2: hi + lo),
+ * *list = per-half selection list length, *split = candidate ranges. */
 int mepol_knn_plan_info(int64_t n_cand, int64_t n_query, int d, int kp1, int split_hint, int* ks,
                         int* list, int* split);
 int mepol_knn(const float* cand, int64_t n_cand, const float* query, int64_t n_query, int d,
@@ -127,10 +142,12 @@ int mepol_rollout_mlp(int env_id, const double* W1, const double* b1, int h0, co
                       size_t workspace_bytes, void* stream);
 /* Scratch for mepol_rollout_mlp's multi-workgroup form (ceil(h1/64) workgroups per trajectory,
  * each holding its 64 columns of W2^T in LDS; used when n * ceil(h1/64) fits the CUs and
- * h0 <= 312).  Word 0 of the workspace is a device int32 error flag: 1 = the workgroups of a
- * trajectory could not all run at once (results invalid; the caller raises).  A null or short
- * workspace selects the one-workgroup-per-trajectory form (same results, bitwise). */
-int mepol_rollout_mlp_workspace_size(int64_t n, int h0, int h1, size_t* bytes);
+ * h0 <= 312): one 8-byte mail word per (trajectory, step, part, action).  Word 0 of the
+ * workspace is a device int32 error flag: 1 = the workgroups of a trajectory could not all run
+ * at once (results invalid; the caller raises).  A null or short workspace selects the
+ * one-workgroup-per-trajectory form (same results, bitwise). */
+int mepol_rollout_mlp_workspace_size(int64_t n, int64_t T, int h0, int h1, int a_dim,
+                                     size_t* bytes);
 
 /* ---- policy MLP (GaussianPolicy, src/policy.py:16-51) for the large-batch passes -----------
  * Gaussian head: mean layer + log-probability with the last hidden layer's bias and ReLU folded

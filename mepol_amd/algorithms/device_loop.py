@@ -162,14 +162,20 @@ class DeviceIteration:
                 == [p.data_ptr() for p in self.params])
 
     def _make_bufs(self, dev):
+        from .._lib import MappedHost
+
         f64 = dict(dtype=torch.float64, device=dev)
-        scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
-        vals_host = torch.zeros(2, dtype=torch.float64).pin_memory()
+        # per-replay scalars in and (H, KL) out: pinned host memory mapped into the device
+        # address space, moved by one-wave kernels (no memcpy nodes in the graph)
+        scal_host = MappedHost(8)
+        vals_host = MappedHost(2)
+        scal_host.np[:] = 0.0
+        vals_host.np[:] = 0.0
         # shadow: theta at the start of the replay = the last accepted parameters (a rejected
         # step is undone by the caller before the next one): off_policy_optimization copies it
         # into last_valid only when it needs it, not after every accepted step
-        return dict(scal=torch.zeros(8, **f64), scal_host=scal_host, scal_np=scal_host.numpy(),
-                    vals=torch.zeros(2, **f64), vals_host=vals_host, vals_np=vals_host.numpy(),
+        return dict(scal=torch.zeros(8, **f64), scal_host=scal_host, scal_np=scal_host.np,
+                    vals=torch.zeros(2, **f64), vals_host=vals_host, vals_np=vals_host.np,
                     shadow=[torch.empty_like(p) for p in self.params], moments=[])
 
     def _use(self, par):
@@ -330,9 +336,8 @@ class DeviceIteration:
         ops.iw_forward(lt, self.logp_b, self.offsets, N, w_out=self.w_cur)
         out2, _, _ = ops.entropy_forward(self.w_cur, self.idx32T, self.D, k, self.ns, self.G,
                                          self.B, self.eps, g_out=self.g_cur)
-        torch.cat((self.out_cur[:1], out2[1:2]), out=self.vals)
-        self.out_cur.copy_(out2)
-        self._vals_out()
+        # (H(theta_t), KL(theta_t+1)) to the host, theta_t+1's sums kept for the next replay
+        ops.scalars_emit(self.out_cur, 0, out2, 1, self.vals_host, self.out_cur, out2, 4)
 
     def _optim_step(self, grads):
         """optimizer.step() (mepol.py:280).  The kernel also leaves theta_t in the replay's
@@ -344,12 +349,10 @@ class DeviceIteration:
         ops.optim_step(self.kind, self.params, grads, self.m, self.v, self.scal, snapshot=snap)
 
     # The replay's scalar inputs (enable flag, lr and bias corrections) come from, and its two
-    # control outputs go to, pinned host buffers through memcpy nodes of the graph itself.
+    # control outputs go to (ops.scalars_emit at the end of _body), mapped pinned host buffers,
+    # moved by one-wave kernels of the graph.
     def _scal_in(self):
-        ops.memcpy_async(self.scal, self.scal_host)
-
-    def _vals_out(self):
-        ops.memcpy_async(self.vals_host, self.vals)
+        ops.small_copy(self.scal, self.scal_host, 8)
 
     @torch.no_grad()
     def _prime(self):

@@ -140,6 +140,9 @@ __global__ void rollout_step_kernel(double* __restrict__ env_f64, float* __restr
 // per-step launch sequence (3 GEMMs + bias/ReLU + rollout_step, ~58 us per step even as a
 // replayed graph) with ~3 barriers per step.
 constexpr int kRollMaxH = 512;
+// mail word not yet published (memset 0xff): a NaN bit pattern no f64 partial sum of the
+// policy's finite weights and activations produces
+constexpr unsigned long long kMailEmpty = ~0ull;
 constexpr int kRollMaxA = 8;
 
 template <int ENV, int KR, int U>
@@ -301,7 +304,7 @@ __global__ __launch_bounds__(64) void rollout_mlp_mw_kernel(
     const float* __restrict__ init32, const double* __restrict__ noise, int64_t n, int64_t T,
     float* __restrict__ states_rec, float* __restrict__ actions_rec,
     double* __restrict__ visited, double* __restrict__ final_state, int np, int nw,
-    unsigned long long* __restrict__ mail, unsigned* __restrict__ flags, int* __restrict__ err) {
+    unsigned long long* __restrict__ mail, int* __restrict__ err) {
   extern __shared__ double sW2[];  // [h0][64]: W2^T rows, this part's 64 columns
   __shared__ double sh1[kRollMaxH];
   const int64_t i = blockIdx.x / np;
@@ -347,7 +350,6 @@ __global__ __launch_bounds__(64) void rollout_mlp_mw_kernel(
     states_rec[(i * (T + 1)) * 2 + 0] = (float)x0;
     states_rec[(i * (T + 1)) * 2 + 1] = (float)x1;
   }
-  unsigned* myflags = flags + i * np;
   __syncthreads();
   for (int64_t t = 0; t < T; ++t) {
     double nz_next[kRollMaxA];
@@ -366,8 +368,10 @@ __global__ __launch_bounds__(64) void rollout_mlp_mw_kernel(
     double acc = 0.0;
     for (int k = 0; k < h0; ++k) acc = fma(sW2[k * 64 + lane], sh1[k], acc);
     const double h2 = c1 ? fmax(acc + bb2, 0.0) : 0.0;
-    // mean layer: this part's wave partial (the shuffle tree of rollout_mlp_kernel), lane 0's
-    unsigned long long* slot = mail + ((i * 2 + (t & 1)) * np) * kRollMaxA;
+    // mean layer: this part's wave partial (the shuffle tree of rollout_mlp_kernel), lane 0's,
+    // published to this step's own mail words (8-B sc1 stores; every word is pre-filled with
+    // kMailEmpty, which no partial can equal, so each word validates itself: no flag, no wait)
+    unsigned long long* slot = mail + (i * T + t) * np * a_dim;
 #pragma unroll
     for (int a = 0; a < kRollMaxA; ++a) {
       if (a < a_dim) {
@@ -375,23 +379,22 @@ __global__ __launch_bounds__(64) void rollout_mlp_mw_kernel(
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m, kWave);
         if (lane == 0)
-          __hip_atomic_store(slot + p * kRollMaxA + a, __double_as_longlong(q), __ATOMIC_RELAXED,
+          __hip_atomic_store(slot + p * a_dim + a, __double_as_longlong(q), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0)
-      __hip_atomic_store(myflags + p, (unsigned)(t + 1), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    // wait for every part's partial of this step (lane q < np polls part q)
+    // every part's partials of this step: lane l < np a_dim polls word l (part l / a_dim,
+    // action l % a_dim) with sc1 loads until it is published
+    double word = 0.0;
     {
+      const int nword = np * a_dim;
       unsigned spins = 0;
       bool bad = false;
+      unsigned long long v = 0;
       while (true) {
-        const bool ok = lane >= np || __hip_atomic_load(myflags + lane, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT) >=
-                                          (unsigned)(t + 1);
-        if (!__ballot(!ok)) break;
+        if (lane < nword)
+          v = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (!__ballot(lane < nword && v == kMailEmpty)) break;
         if (++spins > (1u << 24)) {
           bad = true;
           break;
@@ -402,14 +405,12 @@ __global__ __launch_bounds__(64) void rollout_mlp_mw_kernel(
         if (lane == 0) atomicExch(err, 1);
         return;
       }
+      word = __longlong_as_double(v);
     }
     double act[kRollMaxA];
     for (int a = 0; a < a_dim; ++a) {
-      double mu = __longlong_as_double(
-          __hip_atomic_load(slot + a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      for (int q = 1; q < np; ++q)
-        mu += __longlong_as_double(__hip_atomic_load(slot + q * kRollMaxA + a, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT));
+      double mu = __shfl(word, a, kWave);
+      for (int q = 1; q < np; ++q) mu += __shfl(word, q * a_dim + a, kWave);
       for (int q = np; q < nw; ++q) mu += 0.0;  // rollout_mlp_kernel's waves without columns
       mu += bm[a];
       // output = mean + randn * exp(log_std)   (policy.py:59)
@@ -493,19 +494,20 @@ extern "C" int mepol_rollout_step(int env_id, double* env_f64, float* env_f32, c
 // nf = 2 -> [h0, h1] -> a_dim with ReLU: W1 [h0,2], b1, W2t = W2^T [h0,h1], b2, Wm [a,h1], bm,
 // log_std [a]; noise [T,n,a_dim] f64.  Writes states_rec [n,T+1,2] f32, actions_rec [n,T,a] f32,
 // visited [n,T,2] f64 (nullable), final_state [n,2] f64 (nullable).
-// Multi-workgroup form: mail [n][2][np][kRollMaxA] (8-byte words), flags [n][np], err (word 0).
-static size_t rollout_mw_bytes(int64_t n, int h1) {
+// Multi-workgroup form: err (word 0), then mail [n][T][np][a_dim] 8-byte words (kMailEmpty).
+static size_t rollout_mw_bytes(int64_t n, int64_t T, int h1, int a_dim) {
   const int64_t np = (h1 + 63) / 64;
-  return 256 + align_up((size_t)n * 2 * np * kRollMaxA * 8, 256) + (size_t)n * np * 4;
+  return 256 + (size_t)n * T * np * a_dim * 8;
 }
 static constexpr int kRollMwMaxH0 = 312;  // [h0][64] f64 slice + sh1 within 160 KB of LDS
 
-extern "C" int mepol_rollout_mlp_workspace_size(int64_t n, int h0, int h1, size_t* bytes) {
-  if (n < 0 || h0 <= 0 || h1 <= 0 || !bytes) {
+extern "C" int mepol_rollout_mlp_workspace_size(int64_t n, int64_t T, int h0, int h1, int a_dim,
+                                                size_t* bytes) {
+  if (n < 0 || T < 0 || h0 <= 0 || h1 <= 0 || a_dim <= 0 || a_dim > kRollMaxA || !bytes) {
     set_error("mepol_rollout_mlp_workspace_size: bad arguments");
     return kErrBadArg;
   }
-  *bytes = rollout_mw_bytes(n, h1);
+  *bytes = rollout_mw_bytes(n, T, h1, a_dim);
   return 0;
 }
 
@@ -534,14 +536,14 @@ extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1,
     MEPOL_HIP(hipGetDevice(&dev));
     MEPOL_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const char* mw = getenv("MEPOL_ROLLOUT_MW");
-    if (workspace && workspace_bytes >= rollout_mw_bytes(n, h1) && h0 <= kRollMwMaxH0 &&
-        n * np <= cus && !(mw && mw[0] == '0')) {
+    if (workspace && workspace_bytes >= rollout_mw_bytes(n, T, h1, a_dim) &&
+        h0 <= kRollMwMaxH0 && n * np <= cus && np * a_dim <= 64 && !(mw && mw[0] == '0')) {
       char* ws = (char*)workspace;
       int* err = (int*)ws;
       unsigned long long* mail = (unsigned long long*)(ws + 256);
-      unsigned* flags = (unsigned*)(ws + 256 + align_up((size_t)n * 2 * np * kRollMaxA * 8, 256));
       MEPOL_HIP(hipMemsetAsync(err, 0, sizeof(int), st));
-      MEPOL_HIP(hipMemsetAsync(flags, 0, (size_t)n * np * 4, st));
+      // every mail word starts as kMailEmpty (all ones)
+      MEPOL_HIP(hipMemsetAsync(mail, 0xff, (size_t)n * T * np * a_dim * 8, st));
       const size_t lds = (size_t)h0 * 64 * sizeof(double);
 #define MEPOL_ROLL_MW(E)                                                                         \
   do {                                                                                           \
@@ -554,8 +556,7 @@ extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1,
     }                                                                                            \
     hipLaunchKernelGGL((rollout_mlp_mw_kernel<E>), dim3((unsigned)(n * np)), dim3(64), lds, st, \
                        W1, b1, h0, W2t, b2, h1, Wm, bm, log_std, a_dim, init64, init32, noise, n, \
-                       T, states_rec, actions_rec, visited, final_state, np, nw, mail, flags,    \
-                       err);                                                                     \
+                       T, states_rec, actions_rec, visited, final_state, np, nw, mail, err);     \
   } while (0)
       if (env_id == 0)
         MEPOL_ROLL_MW(0);

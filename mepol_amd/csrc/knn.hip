@@ -30,6 +30,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <climits>
+#include <cmath>
 #include <cstdlib>
 
 namespace mepol {
@@ -168,13 +169,17 @@ constexpr float kPadNorm16 = 60000.f;  // scaled |c|^2 of padding candidates (> 
 
 // apack16[((t*64 + l)*KS16 + s)*16 + {0..7 hi, 8..15 lo}] = A[i = l&31][k = 16 s + 8 (l>>5) + j]
 // of candidate tile t: f<d: -2 sigma x_cf ; f==d: |sigma c|^2 ; else 0.
-// apack16[((t*KS16 + s)*64 + l)*8 + j] = fl16(A[i = l&31][k = 16 s + 8 (l>>5) + j]) of candidate
-// tile t, A = [-2 sigma c, |sigma c|^2, 0...]: each k-step of a tile is 1 KB, one coalesced
-// dwordx4 per lane.  Padding candidates carry a norm above every real value.
+// apack16[(((t*KS16 + s)*nh + u)*64 + l)*8 + j] = half u of A[i = l&31][k = 16 s + 8 (l>>5) + j]
+// of candidate tile t, A = [-2 sigma c, |sigma c|^2, 0...]; u = 0: fl16(A) (hi), u = 1 (nh = 2
+// only): fl16(A - hi) (lo).  Each (k-step, half) of a tile is 1 KB, one coalesced dwordx4 per
+// lane.  Padding candidates carry a norm above every real value.
+// Also writes cpad [n][dp] f32: the candidate rows padded with zeros to dp = a multiple of 32
+// floats (128-B aligned): refine's exact-distance gathers then read whole lines with dwordx4.
 __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X, int64_t n, int d,
-                                                     int KS16, int64_t nct,
+                                                     int KS16, int nh, int64_t nct,
                                                      _Float16* __restrict__ apack,
-                                                     const unsigned* __restrict__ scal) {
+                                                     const unsigned* __restrict__ scal,
+                                                     float* __restrict__ cpad, int dp) {
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (gid >= nct * 64) return;
   const float sg = knn_scale(scal);
@@ -190,9 +195,21 @@ __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X
       const float y = sg * xc[f];
       cn = fmaf(y, y, cn);
     }
+    // this thread's half of the padded row
+    const int half = dp / 2;
+    f32x4* dst = reinterpret_cast<f32x4*>(cpad + c * dp + h * half);
+    for (int f4 = 0; f4 < half / 4; ++f4) {
+      f32x4 v;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int f = h * half + 4 * f4 + u;
+        v[u] = f < d ? xc[f] : 0.f;
+      }
+      dst[f4] = v;
+    }
   }
   for (int s = 0; s < KS16; ++s) {
-    f16x8 hv;
+    f16x8 hv, lv;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int f = 16 * s + 8 * h + j;
@@ -201,20 +218,28 @@ __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X
         v = (f < d) ? -2.f * sg * X[c * d + f] : ((f == d) ? cn : 0.f);
       else
         v = (f == d) ? kPadNorm16 : 0.f;
-      hv[j] = (_Float16)v;
+      _Float16 a, b;
+      split_f16(v, a, b);
+      hv[j] = a;
+      lv[j] = b;
     }
-    *reinterpret_cast<f16x8*>(apack + ((t * KS16 + s) * 64 + l) * 8) = hv;
+    *reinterpret_cast<f16x8*>(apack + (((t * KS16 + s) * nh) * 64 + l) * 8) = hv;
+    if (nh == 2) *reinterpret_cast<f16x8*>(apack + (((t * KS16 + s) * 2 + 1) * 64 + l) * 8) = lv;
   }
 }
 
-// Partial top-LIST lists of every query over its split's tile range.  The candidates are the
-// f16 hi halves of A (pack16_kernel), the queries are split into f16 hi + lo (2^-22 relative),
-// and 2 MFMAs per k-step (A_hi q_hi + A_hi q_lo) accumulate in f32: the value's error is
-// dominated by the candidate rounding, 2^-11 (|c|^2 + 2 |c||q|) (make_plan's e_terms), which
-// refine's certification accounts for.  Only the hi half travels: 1 KB per k-step and tile,
-// half the fragment stream of a split-candidate (hi + lo) selection.
-template <int KS16, int LIST>
-__global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restrict__ apack,
+// Partial top-LIST lists of every query over its split's tile range.  The queries are split into
+// f16 hi + lo (2^-22 relative).  NH = 1 (candidate-hi, the default): the candidates are the f16
+// hi halves of A and 2 MFMAs per k-step (A_hi q_hi + A_hi q_lo) accumulate in f32; the value's
+// error is dominated by the candidate rounding, 2^-11 (|c|^2 + 2 |c||q|), and only the hi half
+// travels (1 KB per k-step and tile).  NH = 2 (split candidates): A_hi and A_lo travel and 3
+// MFMAs per k-step (+ A_lo q_hi) give ~f32-class values, 2 (3 K + 16 + d) 2^-24 (|c|^2 + 2 |c||q|),
+// for data whose neighbour spacing is below the f16 band (make_plan).  refine's certification
+// uses the plan's bound either way.
+// OCC = 3: __launch_bounds__(256, 3) caps the kernel at 168 VGPRs (3 waves per SIMD) for the
+// short-list instances (a few spilled dwords, on the insertion path only).
+template <int KS16, int LIST, int NH, int OCC>
+__global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __restrict__ apack,
                                                        const float* __restrict__ query,
                                                        int64_t nq, int d, int64_t nct, int split,
                                                        int64_t tiles_per_split, int keep,
@@ -285,8 +310,8 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
   // vector-memory op in the loop).  Three buffers, two where a 4-k-step tile and long lists
   // would otherwise reach the 256-VGPR cap (at the cap the asm-load buffers are not safe from
   // register copies).
-  constexpr int NV = KS16;  // dwordx4 per lane per tile: one per k-step
-  constexpr int NB = (KS16 >= 4 && LIST > 32) ? 2 : 3;
+  constexpr int NV = NH * KS16;  // dwordx4 per lane per tile: one per (k-step, half)
+  constexpr int NB = NH == 2 ? (KS16 >= 4 ? 2 : 3) : ((KS16 >= 4 && LIST > 32) ? 2 : 3);
   const f32x4* abase = reinterpret_cast<const f32x4*>(apack) + l;
   f32x4 Bf[NB][NV];
   auto load = [&](f32x4 (&A)[NV], int64_t t) {
@@ -311,9 +336,13 @@ __global__ __launch_bounds__(256) void select16_kernel(const _Float16* __restric
     f32x16 acc = {};
 #pragma unroll
     for (int s = 0; s < KS16; ++s) {
-      const f16x8 ah = __builtin_bit_cast(f16x8, A[s]);
+      const f16x8 ah = __builtin_bit_cast(f16x8, A[NH * s]);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bhi[s], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, blo[s], acc, 0, 0, 0);
+      if constexpr (NH == 2) {
+        const f16x8 al = __builtin_bit_cast(f16x8, A[2 * s + 1]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bhi[s], acc, 0, 0, 0);
+      }
     }
     return acc;
   };
@@ -470,6 +499,30 @@ __device__ __forceinline__ double exact_d2(const float* __restrict__ a, const fl
   return s;
 }
 
+// exact_d2 with b a padded candidate row (16-B aligned, zeros past d, length a multiple of 32):
+// the same operations in the same order, b read as dwordx4.
+__device__ __forceinline__ double exact_d2_pad(const float* __restrict__ a,
+                                               const float* __restrict__ b, int d) {
+  constexpr int kCh = 32;
+  double s = 0.0;
+  for (int f0 = 0; f0 < d; f0 += kCh) {
+    float av[kCh];
+    f32x4 bv[kCh / 4];
+#pragma unroll
+    for (int u = 0; u < kCh / 4; ++u) bv[u] = reinterpret_cast<const f32x4*>(b + f0)[u];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) av[u] = a[min(f0 + u, d - 1)];
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      if (f0 + u < d) {  // uniform condition
+        const double t = __dsub_rn((double)av[u], (double)bv[u >> 2][u & 3]);
+        s = __dadd_rn(s, __dmul_rn(t, t));
+      }
+    }
+  }
+  return s;
+}
+
 // Correctly rounded f64 square root (round-to-nearest-even, as glibc / numpy / sklearn).
 // y0 = sqrt(x) is within 1 ulp; with Y = y/ulp(y) an integer, x/ulp^2 is an integer, so
 // "RN(sqrt x) >= y+"  <=>  x > y*y+  and  "RN(sqrt x) <= y-"  <=>  x <= y-*y; both signs are
@@ -486,8 +539,8 @@ __device__ __forceinline__ double sqrt_rn(double x) {
 
 template <int LIST, int MAXP>
 __global__ __launch_bounds__(256) void refine_kernel(
-    const float* __restrict__ cand, int64_t nc, const float* __restrict__ query, int64_t nq, int d,
-    int kp1, int M, int list_len, const float* __restrict__ lists_v,
+    const float* __restrict__ cpad, int dp, int64_t nc, const float* __restrict__ query,
+    int64_t nq, int d, int kp1, int M, int list_len, const float* __restrict__ lists_v,
     const int* __restrict__ lists_i, const unsigned* __restrict__ cmax_bits, int e_terms,
     double* __restrict__ Dout,
     int64_t* __restrict__ I64, int32_t* __restrict__ I32, int* __restrict__ flag_count,
@@ -635,7 +688,7 @@ __global__ __launch_bounds__(256) void refine_kernel(
   if (l < mcut) {
     const int c = sel[w][l];
     if (c >= 0) {
-      dd = exact_d2(xq, cand + (int64_t)c * d, d);
+      dd = exact_d2_pad(xq, cpad + (int64_t)c * dp, d);
       di = c;
     }
   }
@@ -885,13 +938,15 @@ __global__ void fill_identity_kernel(int* s, int64_t n) {
 // ---------------------------------------------------------------------------------------
 struct Plan {
   int d, kp1, LIST, split, maxp;
+  int dp;         // padded candidate row (floats, multiple of 32) for refine's gathers
   int KS16;       // k-steps of 16: ceil((d + 1) / 16) <= 4
+  int nh;         // candidate halves in the fragments: 1 (hi, default) or 2 (hi + lo)
   int e_terms;    // selection error bound multiplier (refine certification)
   int keep;       // per-half entries behind the union prune bound
   int LIST16;     // per-half select list length
   int M;          // refine input entries per query: 2*split*LIST16
   int64_t nc, nq, nct, nqt, tiles_per_split;
-  size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_part, total;
+  size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_part, off_cpad, total;
 };
 
 static const int kListChoices[] = {8, 16, 24, 32, 40};
@@ -929,12 +984,29 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
       P->LIST16 = v;
       break;
     }
+  // Candidate halves.  The hi-only band E ~ 3 * 2^-11 C^2 must stay small against the
+  // (k+1)-th neighbour distance, ~C^2 (kp1 / nc)^(2/d) for nc points spread over the radius-C
+  // ball: at C3 / C4 / C5 the ratio is ~0.003, for low-dimensional dense data (GridWorld,
+  // MountainCar, d = 2) it exceeds 1 and nearly every query would go to the exhaustive path.
+  // Split candidates (E ~32x smaller) cover those.  MEPOL_KNN_NH=1|2 forces either.
+  {
+    const double band = 3.0 / 2048.0 * std::pow((double)nc / kp1, 2.0 / d);
+    P->nh = band > 0.03 ? 2 : 1;
+    const char* e = getenv("MEPOL_KNN_NH");
+    if (e && (e[0] == '1' || e[0] == '2')) P->nh = e[0] - '0';
+    // split-candidate instances that stay below the 256-VGPR cap
+    const bool fits2 = (P->KS16 <= 3 && P->LIST16 <= (P->KS16 == 3 ? 32 : 40)) ||
+                       (P->KS16 == 4 && P->LIST16 <= 32);
+    if (!fits2) P->nh = 1;
+  }
   // Selection error bound E = e_terms * 2^-24 * (C^2 + 2 C |q|), unscaled, C = max candidate
-  // norm: the f16 rounding of -2 sigma c and of |sigma c|^2 (2^-11 = 2^13 * 2^-24 relative
-  // each: 2^-11 (2 |c||q| + |c|^2)), the query split (2^-22), the 2 K products per output
-  // summed in f32 (<= 2K roundings) and |c|^2 in f32 (d roundings), these small terms x2, and
-  // 64 for the f16 subnormal range.
-  P->e_terms = 8192 + 64 + 2 * (2 * 16 * P->KS16 + 16 + d);
+  // norm.  Candidate-hi: the f16 rounding of -2 sigma c and of |sigma c|^2 (2^-11 = 2^13 * 2^-24
+  // relative each: 2^-11 (2 |c||q| + |c|^2)), the query split (2^-22), the 2 K products per
+  // output summed in f32 (<= 2K roundings) and |c|^2 in f32 (d roundings), these small terms
+  // x2, and 64 for the f16 subnormal range.  Split candidates: 3 K products summed in f32,
+  // operand splitting 3 * 2^-22 = 12 * 2^-24, |c|^2 in f32 (d), x2.
+  P->e_terms = P->nh == 1 ? 8192 + 64 + 2 * (2 * 16 * P->KS16 + 16 + d)
+                          : 2 * (3 * 16 * P->KS16 + 16 + d);
   // the selection's error band (~0.1 at C3) holds a few more candidates around the (k+1)-th
   // than kp1 + 4: refine ranks the approximate top 64 and evaluates those inside the band
   P->LIST = kRefineList;
@@ -952,6 +1024,8 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
     split = (int)std::min<int64_t>(kMaxSplit, std::max<int64_t>(1, (target + P->nqt - 1) /
                                                                       std::max<int64_t>(P->nqt, 1)));
     split = std::max(split, 2);
+    // refine's rank merge takes <= 256 entries per query (2 split LIST16)
+    split = std::min(split, std::max(2, 256 / (2 * P->LIST16)));
     while (split > 1 && P->nct / split < 16) --split;
   }
   split = std::max(1, std::min(split, kMaxSplit));
@@ -965,7 +1039,7 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   }
   size_t off = 0;
   P->off_apack = off;
-  off = align_up(off + (size_t)P->nct * 64 * P->KS16 * 8 * sizeof(_Float16), 256);
+  off = align_up(off + (size_t)P->nct * 64 * P->KS16 * 16 * sizeof(_Float16), 256);  // nh <= 2
   P->off_scalars = off;  // [0] max |c| bits, [1] fallback count, [2] max |q| bits, [4..5] invalid rows
   off = align_up(off + 32, 256);
   const size_t nl = (size_t)std::max<int64_t>(nq, 1) * P->M;
@@ -977,25 +1051,45 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(int), 256);
   P->off_part = off;  // exact fallback: kExactGrid partial lists of <= 64 (f64, int32)
   off = align_up(off + (size_t)kExactGrid * 64 * (sizeof(double) + sizeof(int)), 256);
+  P->dp = (d + 31) / 32 * 32;
+  P->off_cpad = off;
+  off = align_up(off + (size_t)nc * P->dp * sizeof(float), 256);
   P->total = off;
   return 0;
 }
 
-template <int KS16>
+static int select_occ3() {
+  const char* e = getenv("MEPOL_KNN_OCC3");
+  return !(e && e[0] == '0');
+}
+
+template <int KS16, int NH>
 static void launch_select16_ks(const Plan& P, const _Float16* ap, const float* query,
                                const unsigned* scal, float* lv, int* li, hipStream_t st) {
   const dim3 g((unsigned)((P.nqt + 3) / 4), (unsigned)P.split);
-#define MEPOL_SEL16(L)                                                                           \
-  hipLaunchKernelGGL((select16_kernel<KS16, L>), g, dim3(256), 0, st, ap, query, P.nq, P.d,       \
-                     P.nct, P.split, P.tiles_per_split, P.keep, scal, lv, li)
-  switch (P.LIST16) {  // >= keep + 4 >= 7
+#define MEPOL_SEL16O(L, O)                                                                       \
+  hipLaunchKernelGGL((select16_kernel<KS16, L, NH, O>), g, dim3(256), 0, st, ap, query, P.nq,     \
+                     P.d, P.nct, P.split, P.tiles_per_split, P.keep, scal, lv, li)
+#define MEPOL_SEL16(L) MEPOL_SEL16O(L, 1)
+  switch (P.LIST16) {  // >= keep + 4 >= 7; split-candidate plans keep the instances that fit
     case 8: MEPOL_SEL16(8); break;
     case 16: MEPOL_SEL16(16); break;
-    case 24: MEPOL_SEL16(24); break;
+    case 24:
+      if constexpr (NH == 1 && KS16 <= 2) {
+        if (select_occ3()) {
+          MEPOL_SEL16O(24, 3);
+          break;
+        }
+      }
+      MEPOL_SEL16(24);
+      break;
     case 32: MEPOL_SEL16(32); break;
-    default: MEPOL_SEL16(40); break;
+    default:
+      if constexpr (NH == 1 || KS16 <= 2) MEPOL_SEL16(40);
+      break;
   }
 #undef MEPOL_SEL16
+#undef MEPOL_SEL16O
 }
 
 // MEPOL_KNN_RANK_MERGE=0 selects the argmin-round merge in refine_kernel (A/B probe).
@@ -1007,15 +1101,15 @@ static int refine_rank_merge() {
   return v;
 }
 
-static void launch_refine(const Plan& P, const float* cand, const float* query, const float* lv,
+static void launch_refine(const Plan& P, const float* cpad, const float* query, const float* lv,
                           const int* li, const unsigned* cmax, double* D, int64_t* I64,
                           int32_t* I32, int* fc, int* fl, hipStream_t st) {
   dim3 g((unsigned)((P.nq + 3) / 4));
   // MAXP = ceil(M / 64) <= 32
 #define MEPOL_REFINE(MP)                                                                          \
-  hipLaunchKernelGGL((refine_kernel<kRefineList, MP>), g, dim3(256), 0, st, cand, P.nc, query,    \
-                     P.nq, P.d, P.kp1, P.M, P.LIST16, lv, li, cmax, P.e_terms, D, I64, I32, fc,   \
-                     fl, refine_rank_merge())
+  hipLaunchKernelGGL((refine_kernel<kRefineList, MP>), g, dim3(256), 0, st, cpad, P.dp, P.nc,     \
+                     query, P.nq, P.d, P.kp1, P.M, P.LIST16, lv, li, cmax, P.e_terms, D, I64,     \
+                     I32, fc, fl, refine_rank_merge())
   if (P.maxp <= 2)
     MEPOL_REFINE(2);
   else if (P.maxp <= 4)
@@ -1082,7 +1176,7 @@ extern "C" int mepol_knn_plan_info(int64_t n_cand, int64_t n_query, int d, int k
   Plan P;
   int rc = make_plan(n_cand, n_query, d, kp1, split_hint, &P);
   if (rc) return rc;
-  if (ks) *ks = P.KS16;
+  if (ks) *ks = P.KS16 * 10 + P.nh;  // k-steps of 16, candidate halves
   if (list) *list = P.LIST16;
   if (split) *split = P.split;
   return 0;
@@ -1114,6 +1208,7 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
   int* flist = (int*)(ws + P.off_flag);
   double* pd = (double*)(ws + P.off_part);
   int* pi = (int*)(ws + P.off_part + (size_t)kExactGrid * 64 * sizeof(double));
+  float* cpad = (float*)(ws + P.off_cpad);
   MEPOL_HIP(hipMemsetAsync(ws + P.off_scalars, 0, 32, st));
   if (n_fallback_out) MEPOL_HIP(hipMemsetAsync(n_fallback_out, 0, sizeof(int32_t), st));
   // scal[0] = max candidate norm (refine's C), scal[2] = max query norm (f16 scale)
@@ -1139,16 +1234,25 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
   }
   const int64_t total = P.nct * 64;
   hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, cand,
-                     P.nc, P.d, P.KS16, P.nct, ap16, cmax);
+                     P.nc, P.d, P.KS16, P.nh, P.nct, ap16, cmax, cpad, P.dp);
   MEPOL_CHECK_LAUNCH();
-  switch (P.KS16) {
-    case 1: launch_select16_ks<1>(P, ap16, query, cmax, lv, li, st); break;
-    case 2: launch_select16_ks<2>(P, ap16, query, cmax, lv, li, st); break;
-    case 3: launch_select16_ks<3>(P, ap16, query, cmax, lv, li, st); break;
-    default: launch_select16_ks<4>(P, ap16, query, cmax, lv, li, st); break;
+  if (P.nh == 1) {
+    switch (P.KS16) {
+      case 1: launch_select16_ks<1, 1>(P, ap16, query, cmax, lv, li, st); break;
+      case 2: launch_select16_ks<2, 1>(P, ap16, query, cmax, lv, li, st); break;
+      case 3: launch_select16_ks<3, 1>(P, ap16, query, cmax, lv, li, st); break;
+      default: launch_select16_ks<4, 1>(P, ap16, query, cmax, lv, li, st); break;
+    }
+  } else {
+    switch (P.KS16) {
+      case 1: launch_select16_ks<1, 2>(P, ap16, query, cmax, lv, li, st); break;
+      case 2: launch_select16_ks<2, 2>(P, ap16, query, cmax, lv, li, st); break;
+      case 3: launch_select16_ks<3, 2>(P, ap16, query, cmax, lv, li, st); break;
+      default: launch_select16_ks<4, 2>(P, ap16, query, cmax, lv, li, st); break;
+    }
   }
   MEPOL_CHECK_LAUNCH();
-  launch_refine(P, cand, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st);
+  launch_refine(P, cpad, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st);
   MEPOL_CHECK_LAUNCH();
   launch_exact_kp1(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, kExactGrid, st,
                    pd, pi);

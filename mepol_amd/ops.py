@@ -77,7 +77,7 @@ def knn_plan(n_cand, n_query, d, kp1, split=0):
     ks, lst, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     call("mepol_knn_plan_info", n_cand, n_query, d, kp1, split, ctypes.byref(ks),
          ctypes.byref(lst), ctypes.byref(sp))
-    return {"KS16": ks.value, "LIST16": lst.value, "split": sp.value}
+    return {"KS16": ks.value // 10, "nh": ks.value % 10, "LIST16": lst.value, "split": sp.value}
 
 
 def knn(cand, kp1, query=None, split=0, want_int64=True, return_fallback=False):
@@ -408,7 +408,7 @@ def rollout_mlp(env_id, W1, b1, W2, b2, Wm, bm, log_std, init, noise, states_rec
     import ctypes
 
     nbytes = ctypes.c_size_t()
-    call("mepol_rollout_mlp_workspace_size", n, h0, h1, ctypes.byref(nbytes))
+    call("mepol_rollout_mlp_workspace_size", n, T, h0, h1, a_dim, ctypes.byref(nbytes))
     ws = _workspace(init.device, nbytes.value, tag="rollout")
     call("mepol_rollout_mlp", env_id, ptr(W1.contiguous()), ptr(b1), h0, ptr(W2t), ptr(b2), h1,
          ptr(Wm.contiguous()), ptr(bm), ptr(log_std.contiguous()), a_dim, ptr(init64), ptr(init32),
@@ -418,6 +418,17 @@ def rollout_mlp(env_id, W1, b1, W2, b2, Wm, bm, log_std, init, noise, states_rec
     if int(ws[:4].view(torch.int32)[0].item()) != 0:
         raise _lib.MepolError("mepol_rollout_mlp: the workgroups of a trajectory were not co-resident "
                          "(MEPOL_ROLLOUT_MW=0 selects the one-workgroup form)")
+
+
+def small_copy(dst, src, n, to_host=False):
+    """dst[:n] <- src[:n] (f64, n <= 64) by a one-wave kernel, on the current stream; src (or
+    dst, to_host=True) is a _lib.MappedHost (a kernel node in a captured graph, no memcpy node)."""
+    call("mepol_small_copy", ptr(dst), ptr(src), n, int(to_host), _stream())
+
+
+def scalars_emit(a, ia, b, ib, vals, cur, nw, n):
+    """vals[0] = a[ia], vals[1] = b[ib]; then cur[:n] = nw[:n] (one launch)."""
+    call("mepol_scalars_emit", ptr(a), ia, ptr(b), ib, ptr(vals), ptr(cur), ptr(nw), n, _stream())
 
 
 def memcpy_async(dst, src):

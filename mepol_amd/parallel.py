@@ -391,8 +391,24 @@ class ShardedIteration(DeviceIteration):
         self.forward()
         sums = self._fwd_exchange()
         torch.stack((self.B - self.sums_cur[0], sums[1] / self.N_global), out=self.vals)
-        self.sums_cur.copy_(sums)
-        self._vals_out()
+        ops.scalars_emit(self.vals, 0, self.vals, 1, self.vals_host, self.sums_cur, sums, 2)
+
+    def step(self, speculate=False):
+        H, KL = super().step(speculate)
+        if os.environ.get("MEPOL_CHECK_RANKS") == "1":
+            self.check_ranks_agree(H, KL)
+        return H, KL
+
+    def check_ranks_agree(self, H, KL):
+        """Debug mode (MEPOL_CHECK_RANKS=1): every rank must read bit-identical (H, KL), or the
+        ranks could take different accept / backtrack branches and, after a cancel(), issue
+        different collective sequences.  All-gathers the bit patterns (NaN-safe) and raises."""
+        bits = torch.tensor([H, KL], dtype=torch.float64, device=self.device).view(torch.int64)
+        allb = torch.empty(self.world * 2, dtype=torch.int64, device=self.device)
+        self.dist.all_gather_into_tensor(allb, bits, group=self.group)
+        rows = allb.view(self.world, 2).cpu()
+        if not bool((rows == rows[0]).all()):
+            raise RuntimeError(f"ranks disagree on (H, KL): {rows.view(torch.float64).tolist()}")
 
     def try_capture(self):
         """Capture the iteration; all ranks agree on graph or eager.  The warm-up pass issues

@@ -77,6 +77,7 @@ def _run(dist, graph, monkeypatch, kl_threshold=10.0, lr=1e-3):
 
 @pytest.mark.parametrize("kl_threshold,lr", [(10.0, 1e-3), (1e-3, 5e-2)])
 def test_sharded_graph_matches_eager(cuda, nccl_world1, monkeypatch, kl_threshold, lr):
+    monkeypatch.setenv("MEPOL_CHECK_RANKS", "1")  # the debug cross-rank (H, KL) agreement check
     g = _run(nccl_world1, True, monkeypatch, kl_threshold, lr)
     e = _run(nccl_world1, False, monkeypatch, kl_threshold, lr)
     assert g["graph"], "the sharded iteration was not captured"
