@@ -158,8 +158,8 @@ class _EmulatedDist:
         o = out.view(self.world, -1)
         flat = inp.reshape(-1)
         o[0].copy_(flat)
-        pe = self.peers
-        src = pe if (pe and pe[0].shape == inp.shape and pe[0].dtype == inp.dtype) else None
+        pe = self.peers  # ShardedEpoch gathers flattened tensors: match by size and dtype
+        src = pe if (pe and pe[0].numel() == inp.numel() and pe[0].dtype == inp.dtype) else None
         for r in range(1, self.world):
             o[r].copy_(src[r - 1].reshape(-1) if src is not None else flat)
 

@@ -130,6 +130,7 @@ class DeviceIteration:
         # shadow of theta and a snapshot of the optimizer moments taken before its step, so a
         # speculative replay can be undone (cancel) when replay t turns out rejected.
         self.speculative = os.environ.get("MEPOL_SPECULATE", "1") != "0"
+        self.mapped = os.environ.get("MEPOL_MAPPED_SCALARS", "0") == "1"
         self._bufs = [self._make_bufs(dev) for _ in range(2 if self.speculative else 1)]
         self._use(0)
         self._inflight = []   # parities launched and not yet returned by step(), oldest first
@@ -165,17 +166,24 @@ class DeviceIteration:
         from .._lib import MappedHost
 
         f64 = dict(dtype=torch.float64, device=dev)
-        # per-replay scalars in and (H, KL) out: pinned host memory mapped into the device
-        # address space, moved by one-wave kernels (no memcpy nodes in the graph)
-        scal_host = MappedHost(8)
-        vals_host = MappedHost(2)
-        scal_host.np[:] = 0.0
-        vals_host.np[:] = 0.0
+        # per-replay scalars in and (H, KL) out.  MEPOL_MAPPED_SCALARS=1: pinned host memory
+        # mapped into the device address space, moved by one-wave kernels (no memcpy nodes in
+        # the graph); default: pinned host tensors behind graph memcpy nodes.
+        if self.mapped:
+            scal_host = MappedHost(8)
+            vals_host = MappedHost(2)
+            scal_host.np[:] = 0.0
+            vals_host.np[:] = 0.0
+            scal_np, vals_np = scal_host.np, vals_host.np
+        else:
+            scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
+            vals_host = torch.zeros(2, dtype=torch.float64).pin_memory()
+            scal_np, vals_np = scal_host.numpy(), vals_host.numpy()
         # shadow: theta at the start of the replay = the last accepted parameters (a rejected
         # step is undone by the caller before the next one): off_policy_optimization copies it
         # into last_valid only when it needs it, not after every accepted step
-        return dict(scal=torch.zeros(8, **f64), scal_host=scal_host, scal_np=scal_host.np,
-                    vals=torch.zeros(2, **f64), vals_host=vals_host, vals_np=vals_host.np,
+        return dict(scal=torch.zeros(8, **f64), scal_host=scal_host, scal_np=scal_np,
+                    vals=torch.zeros(2, **f64), vals_host=vals_host, vals_np=vals_np,
                     shadow=[torch.empty_like(p) for p in self.params], moments=[])
 
     def _use(self, par):
@@ -337,7 +345,7 @@ class DeviceIteration:
         out2, _, _ = ops.entropy_forward(self.w_cur, self.idx32T, self.D, k, self.ns, self.G,
                                          self.B, self.eps, g_out=self.g_cur)
         # (H(theta_t), KL(theta_t+1)) to the host, theta_t+1's sums kept for the next replay
-        ops.scalars_emit(self.out_cur, 0, out2, 1, self.vals_host, self.out_cur, out2, 4)
+        self._emit(self.out_cur, 0, out2, 1, self.out_cur, out2, 4)
 
     def _optim_step(self, grads):
         """optimizer.step() (mepol.py:280).  The kernel also leaves theta_t in the replay's
@@ -352,7 +360,21 @@ class DeviceIteration:
     # control outputs go to (ops.scalars_emit at the end of _body), mapped pinned host buffers,
     # moved by one-wave kernels of the graph.
     def _scal_in(self):
-        ops.small_copy(self.scal, self.scal_host, 8)
+        if self.mapped:
+            ops.small_copy(self.scal, self.scal_host, 8)
+        else:
+            ops.memcpy_async(self.scal, self.scal_host)
+
+    def _emit(self, a, ia, b, ib, cur, nw, n):
+        """vals_host <- (a[ia], b[ib]); cur[:n] <- nw[:n] (mepol_scalars_emit, or the torch
+        copies + a memcpy node)."""
+        if self.mapped:
+            ops.scalars_emit(a, ia, b, ib, self.vals_host, cur, nw, n)
+            return
+        if not (a is self.vals and b is self.vals and (ia, ib) == (0, 1)):
+            torch.stack((a[ia], b[ib]), out=self.vals)
+        cur[:n].copy_(nw[:n])
+        ops.memcpy_async(self.vals_host, self.vals)
 
     @torch.no_grad()
     def _prime(self):

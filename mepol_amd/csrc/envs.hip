@@ -364,9 +364,36 @@ __global__ __launch_bounds__(64) void rollout_mlp_mw_kernel(
                       0.0);
     }
     __syncthreads();
-    // layer 2, this part's columns: h2_j = relu(sum_k W2[j][k] h1[k] + b2[j]), k in order
+    // layer 2, this part's columns: h2_j = relu(sum_k W2[j][k] h1[k] + b2[j]), k in order (one
+    // fma chain); the LDS operands of rows k+8 .. k+15 are loaded while rows k .. k+7 are summed
     double acc = 0.0;
-    for (int k = 0; k < h0; ++k) acc = fma(sW2[k * 64 + lane], sh1[k], acc);
+    {
+      constexpr int U = 8;
+      double wc[U], hc[U], wn[U], hn[U];
+      auto fetch = [&](double (&w)[U], double (&h)[U], int k0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int k = min(k0 + u, h0 - 1);  // clamped: rows past h0 are never summed
+          w[u] = sW2[k * 64 + lane];
+          h[u] = sh1[k];
+        }
+      };
+      fetch(wc, hc, 0);
+      int k = 0;
+      for (; k + U <= h0; k += U) {
+        fetch(wn, hn, k + U);
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc = fma(wc[u], hc[u], acc);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          wc[u] = wn[u];
+          hc[u] = hn[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (k + u < h0) acc = fma(wc[u], hc[u], acc);
+    }
     const double h2 = c1 ? fmax(acc + bb2, 0.0) : 0.0;
     // mean layer: this part's wave partial (the shuffle tree of rollout_mlp_kernel), lane 0's,
     // published to this step's own mail words (8-B sc1 stores; every word is pre-filled with

@@ -391,7 +391,7 @@ class ShardedIteration(DeviceIteration):
         self.forward()
         sums = self._fwd_exchange()
         torch.stack((self.B - self.sums_cur[0], sums[1] / self.N_global), out=self.vals)
-        ops.scalars_emit(self.vals, 0, self.vals, 1, self.vals_host, self.sums_cur, sums, 2)
+        self._emit(self.vals, 0, self.vals, 1, self.sums_cur, sums, 2)
 
     def step(self, speculate=False):
         H, KL = super().step(speculate)

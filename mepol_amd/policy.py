@@ -80,8 +80,6 @@ class _HeadLogp(torch.autograd.Function):
 class _TwoLayerLogp(torch.autograd.Function):
     """log p(a | s) of the reference's 2-hidden-layer ReLU policy for a large batch:
 
-    fused    h1, z2 and the head in ONE kernel (csrc/policy_fwd.hip) when nf <= 64, h1 <= 320;
-             otherwise the three steps below
     fused    layer 1, layer 2 and the head in ONE kernel (csrc/policy_fwd.hip) when nf <= 64
              and h1 <= 320; otherwise the three steps:
     layer 1  h1 = relu(x W1^T + b1)            HIP (csrc/mlp.hip), bias + ReLU fused

@@ -52,7 +52,7 @@ def test_emulated_dist_fills_peer_slots():
     own = torch.arange(6, dtype=torch.float32).reshape(3, 2)
     d.peers = [torch.full((3, 2), float(r)) for r in (1, 2, 3)]
     out = torch.empty(4 * 6, dtype=torch.float32)
-    d.all_gather_into_tensor(out, own)
+    d.all_gather_into_tensor(out, own.reshape(-1))    # ShardedEpoch passes flattened payloads
     o = out.view(4, 3, 2)
     assert torch.equal(o[0], own) and all(bool((o[r] == r).all()) for r in (1, 2, 3))
     w = torch.arange(5, dtype=torch.float64)
