@@ -39,19 +39,7 @@ const char* mepol_last_error_string(void);
 int mepol_abi_version(void);
 /* Stream-ordered copy (device <-> pinned host / device); captured as a graph memcpy node. */
 int mepol_memcpy_async(void* dst, const void* src, size_t bytes, void* stream);
-/* Pinned host memory mapped into the device address space (hipHostMallocMapped): the host
- * reads / writes it at *host_ptr, kernels at *dev_ptr.  Used for the per-replay scalars of the
- * captured off-policy iteration (no memcpy nodes in the graph). */
-int mepol_host_alloc_mapped(size_t bytes, void** host_ptr, void** dev_ptr);
-int mepol_host_free(void* host_ptr);
-/* dst[0..n) = src[0..n), n <= 64 f64, one wave; to_host = 0: src is mapped host memory
- * (mepol_host_alloc_mapped), 1: dst is.  The mapped side is accessed at system scope. */
-int mepol_small_copy(double* dst, const double* src, int n, int to_host, void* stream);
-/* vals[0] = a[ia], vals[1] = b[ib] (both read first), then cur[0..n) = nw[0..n), n <= 64:
- * the iteration's control outputs (H(theta_t), KL(theta_t+1)) to mapped host memory and the
- * next replay's entropy sums, in one launch (mepol.py:429-439 reads these two scalars). */
-int mepol_scalars_emit(const double* a, int ia, const double* b, int ib, double* vals,
-                       double* cur, const double* nw, int n, void* stream);
+
 
 /* ---- k-NN ---------------------------------------------------------------------------------
  * Replaces src/algorithms/mepol.py:190-192

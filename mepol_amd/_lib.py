@@ -66,10 +66,6 @@ SIGNATURES = {
     "mepol_rollout_mlp_workspace_size": [_c_i64, _c_i64, _c_int, _c_int, _c_int,
                                          ctypes.POINTER(_c_sz)],
     "mepol_memcpy_async": [_c_vp, _c_vp, _c_sz, _c_vp],
-    "mepol_host_alloc_mapped": [_c_sz, ctypes.POINTER(_c_vp), ctypes.POINTER(_c_vp)],
-    "mepol_host_free": [_c_vp],
-    "mepol_small_copy": [_c_vp, _c_vp, _c_int, _c_int, _c_vp],
-    "mepol_scalars_emit": [_c_vp, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_vp, _c_int, _c_vp],
     "mepol_optim_step": [_c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
     "mepol_optim_step_snapshot": [_c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
                                   _c_vp, _c_vp, _c_vp, _c_vp],
@@ -118,30 +114,6 @@ def call(name, *args):
         cls = MepolInputError if rc == 1001 else MepolError
         raise cls(f"{name} failed (rc={rc}): {msg.decode() if msg else ''}")
     return rc
-
-
-class MappedHost:
-    """n f64 of pinned host memory mapped into the device address space: the host reads and
-    writes `.np` (a numpy view), kernels take `.dev` (data_ptr() is the device address, so it
-    passes through ptr() like a tensor)."""
-
-    def __init__(self, n):
-        import numpy as np
-
-        h, d = ctypes.c_void_p(), ctypes.c_void_p()
-        call("mepol_host_alloc_mapped", n * 8, ctypes.byref(h), ctypes.byref(d))
-        self.host, self.dev, self.n = h.value, d.value, n
-        self.np = np.ctypeslib.as_array((ctypes.c_double * n).from_address(self.host))
-        self._free = load().mepol_host_free
-
-    def data_ptr(self):
-        return self.dev
-
-    def __del__(self):
-        try:
-            self._free(ctypes.c_void_p(self.host))
-        except Exception:  # interpreter shutdown
-            pass
 
 
 def ptr(t):

@@ -130,7 +130,6 @@ class DeviceIteration:
         # shadow of theta and a snapshot of the optimizer moments taken before its step, so a
         # speculative replay can be undone (cancel) when replay t turns out rejected.
         self.speculative = os.environ.get("MEPOL_SPECULATE", "1") != "0"
-        self.mapped = os.environ.get("MEPOL_MAPPED_SCALARS", "0") == "1"
         self._bufs = [self._make_bufs(dev) for _ in range(2 if self.speculative else 1)]
         self._use(0)
         self._inflight = []   # parities launched and not yet returned by step(), oldest first
@@ -163,22 +162,11 @@ class DeviceIteration:
                 == [p.data_ptr() for p in self.params])
 
     def _make_bufs(self, dev):
-        from .._lib import MappedHost
-
         f64 = dict(dtype=torch.float64, device=dev)
-        # per-replay scalars in and (H, KL) out.  MEPOL_MAPPED_SCALARS=1: pinned host memory
-        # mapped into the device address space, moved by one-wave kernels (no memcpy nodes in
-        # the graph); default: pinned host tensors behind graph memcpy nodes.
-        if self.mapped:
-            scal_host = MappedHost(8)
-            vals_host = MappedHost(2)
-            scal_host.np[:] = 0.0
-            vals_host.np[:] = 0.0
-            scal_np, vals_np = scal_host.np, vals_host.np
-        else:
-            scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
-            vals_host = torch.zeros(2, dtype=torch.float64).pin_memory()
-            scal_np, vals_np = scal_host.numpy(), vals_host.numpy()
+        # per-replay scalars in and (H, KL) out: pinned host tensors behind graph memcpy nodes
+        scal_host = torch.zeros(8, dtype=torch.float64).pin_memory()
+        vals_host = torch.zeros(2, dtype=torch.float64).pin_memory()
+        scal_np, vals_np = scal_host.numpy(), vals_host.numpy()
         # shadow: theta at the start of the replay = the last accepted parameters (a rejected
         # step is undone by the caller before the next one): off_policy_optimization copies it
         # into last_valid only when it needs it, not after every accepted step
@@ -357,20 +345,12 @@ class DeviceIteration:
         ops.optim_step(self.kind, self.params, grads, self.m, self.v, self.scal, snapshot=snap)
 
     # The replay's scalar inputs (enable flag, lr and bias corrections) come from, and its two
-    # control outputs go to (ops.scalars_emit at the end of _body), mapped pinned host buffers,
-    # moved by one-wave kernels of the graph.
+    # control outputs go to, pinned host buffers through memcpy nodes of the graph itself.
     def _scal_in(self):
-        if self.mapped:
-            ops.small_copy(self.scal, self.scal_host, 8)
-        else:
-            ops.memcpy_async(self.scal, self.scal_host)
+        ops.memcpy_async(self.scal, self.scal_host)
 
     def _emit(self, a, ia, b, ib, cur, nw, n):
-        """vals_host <- (a[ia], b[ib]); cur[:n] <- nw[:n] (mepol_scalars_emit, or the torch
-        copies + a memcpy node)."""
-        if self.mapped:
-            ops.scalars_emit(a, ia, b, ib, self.vals_host, cur, nw, n)
-            return
+        """vals_host <- (a[ia], b[ib]) through a memcpy node; cur[:n] <- nw[:n]."""
         if not (a is self.vals and b is self.vals and (ia, ib) == (0, 1)):
             torch.stack((a[ia], b[ib]), out=self.vals)
         cur[:n].copy_(nw[:n])

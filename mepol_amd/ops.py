@@ -420,17 +420,6 @@ def rollout_mlp(env_id, W1, b1, W2, b2, Wm, bm, log_std, init, noise, states_rec
                          "(MEPOL_ROLLOUT_MW=0 selects the one-workgroup form)")
 
 
-def small_copy(dst, src, n, to_host=False):
-    """dst[:n] <- src[:n] (f64, n <= 64) by a one-wave kernel, on the current stream; src (or
-    dst, to_host=True) is a _lib.MappedHost (a kernel node in a captured graph, no memcpy node)."""
-    call("mepol_small_copy", ptr(dst), ptr(src), n, int(to_host), _stream())
-
-
-def scalars_emit(a, ia, b, ib, vals, cur, nw, n):
-    """vals[0] = a[ia], vals[1] = b[ib]; then cur[:n] = nw[:n] (one launch)."""
-    call("mepol_scalars_emit", ptr(a), ia, ptr(b), ib, ptr(vals), ptr(cur), ptr(nw), n, _stream())
-
-
 def memcpy_async(dst, src):
     """dst <- src (same byte size; device or pinned host tensors), ordered on the current
     stream; inside a graph capture this is a memcpy node."""
