@@ -130,12 +130,18 @@ int mepol_rollout_mlp(int env_id, const double* W1, const double* b1, int h0, co
                       size_t workspace_bytes, void* stream);
 /* Scratch for mepol_rollout_mlp's multi-workgroup form (ceil(h1/64) workgroups per trajectory,
  * each holding its 64 columns of W2^T in LDS; used when n * ceil(h1/64) fits the CUs and
- * h0 <= 312): one 8-byte mail word per (trajectory, step, part, action).  Word 0 of the
+ * h0 <= 306): one 8-byte mail word per (trajectory, step, part, action).  Word 0 of the
  * workspace is a device int32 error flag: 1 = the workgroups of a trajectory could not all run
  * at once (results invalid; the caller raises).  A null or short workspace selects the
- * one-workgroup-per-trajectory form (same results, bitwise). */
+ * one-workgroup-per-trajectory form. */
 int mepol_rollout_mlp_workspace_size(int64_t n, int64_t T, int h0, int h1, int a_dim,
                                      size_t* bytes);
+/* Which form mepol_rollout_mlp takes for this shape (given a sufficient workspace): workgroups
+ * per trajectory, and k_chunks = the number of k-ranges the second layer's sum is split into
+ * (1: one fma chain over all h0 rows; 4: four chains of ceil(h0/4) rows added in order), i.e.
+ * the summation order of oracle/native/rollout_kordered.c the results match bit for bit. */
+int mepol_rollout_mlp_plan_info(int64_t n, int h0, int h1, int a_dim, int* workgroups_per_traj,
+                                int* k_chunks);
 
 /* ---- policy MLP (GaussianPolicy, src/policy.py:16-51) for the large-batch passes -----------
  * Gaussian head: mean layer + log-probability with the last hidden layer's bias and ReLU folded

@@ -65,6 +65,8 @@ SIGNATURES = {
                           _c_vp, _c_sz, _c_vp],
     "mepol_rollout_mlp_workspace_size": [_c_i64, _c_i64, _c_int, _c_int, _c_int,
                                          ctypes.POINTER(_c_sz)],
+    "mepol_rollout_mlp_plan_info": [_c_i64, _c_int, _c_int, _c_int, ctypes.POINTER(_c_int),
+                                    ctypes.POINTER(_c_int)],
     "mepol_memcpy_async": [_c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_optim_step": [_c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
     "mepol_optim_step_snapshot": [_c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,

@@ -284,19 +284,26 @@ __global__ __launch_bounds__(kRollMaxH) void rollout_mlp_kernel(
 
 // ---- whole rollout, several workgroups per trajectory --------------------------------------
 // rollout_mlp_kernel puts a trajectory on ONE CU, which then streams most of W2^T from L2 every
-// step (11.7 us per step at C2's [300, 300]).  Here NP = ceil(h1 / 64) single-wave workgroups
-// share a trajectory: workgroup p owns hidden-2 columns [64 p, 64 p + 64) -- exactly wave p of
-// rollout_mlp_kernel -- and keeps their W2^T slice ([h0][64] f64, <= 156 KB) in LDS for all T
-// steps.  Per step every workgroup computes layer 1 (all h0 columns, redundantly), its 64
-// layer-2 columns (k-ordered fma chain) and its wave partial of the mean layer (the same
-// shuffle tree); the NP partials are exchanged through global memory (sc1 stores, a per-part
-// step flag behind s_waitcnt vmcnt(0), sc1 polls and loads: MI355X_MICROARCH.md's first
-// hand-off row) and every lane of every workgroup sums them in part order, adds the noise and
-// steps the env.  Same operations in the same order as rollout_mlp_kernel: bitwise identical
-// results.  Needs all n * NP workgroups resident at once (one per CU): the host launches it only
-// when n * NP <= the CU count; the flag polls are bounded (err = 1 instead of a hang).
-template <int ENV>
-__global__ __launch_bounds__(64) void rollout_mlp_mw_kernel(
+// step (11.7 us per step at C2's [300, 300]).  Here NP = ceil(h1 / 64) workgroups share a
+// trajectory: workgroup p owns hidden-2 columns [64 p, 64 p + 64) and keeps their W2^T slice
+// ([h0][64] f64, <= 154 KB) in LDS for all T steps.  Per step:
+//   layer 1   all h0 columns (redundantly in every workgroup), 256 threads;
+//   layer 2   its 64 columns; wave w of the 4 sums rows k in [w L, w L + L), L = ceil(h0 / 4), as
+//             one fma chain (a single chain over 300 rows was 5.6 of the 8.4 us step:
+//             tools/rollout_probe.py), and the column total is ((c0 + c1) + c2) + c3;
+//   mean      wave 0's partial of the mean layer over its 64 columns (xor shuffle tree),
+//             published as NP * a_dim self-validating 8-byte mail words (sc1 stores) and polled
+//             with sc1 loads by wave 0 of every workgroup of the trajectory (bounded: err = 1);
+//   env       every thread sums the NP partials in part order, adds bm and the noise and steps
+//             the env (the same state in every thread).
+// The order is oracle/native/rollout_kordered.c's with k_chunks = 4 (mepol_rollout_mlp_plan_info
+// reports it).  Needs all n * NP workgroups resident at once (one per CU by LDS): the host
+// launches it only when n * NP <= the CU count.
+// PROBE (tools/variants/rollout_probe.hip only): thread 0 of each workgroup accumulates
+// s_memtime spans of the step's phases into probe[blockIdx.x][8]; the product has PROBE = false.
+constexpr int kRollMwWaves = 4;
+template <int ENV, bool PROBE = false>
+__global__ __launch_bounds__(64 * kRollMwWaves) void rollout_mlp_mw_kernel(
     const double* __restrict__ W1, const double* __restrict__ b1, int h0,
     const double* __restrict__ W2t, const double* __restrict__ b2, int h1,
     const double* __restrict__ Wm, const double* __restrict__ bm,
@@ -304,34 +311,53 @@ __global__ __launch_bounds__(64) void rollout_mlp_mw_kernel(
     const float* __restrict__ init32, const double* __restrict__ noise, int64_t n, int64_t T,
     float* __restrict__ states_rec, float* __restrict__ actions_rec,
     double* __restrict__ visited, double* __restrict__ final_state, int np, int nw,
-    unsigned long long* __restrict__ mail, int* __restrict__ err) {
+    unsigned long long* __restrict__ mail, int* __restrict__ err, long long* __restrict__ probe) {
   extern __shared__ double sW2[];  // [h0][64]: W2^T rows, this part's 64 columns
   __shared__ double sh1[kRollMaxH];
+  __shared__ double spart[kRollMwWaves][64];
+  __shared__ double sword[64];
+  __shared__ int sbad;
+  long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt = 0;
+  auto stamp = [&](int k, double dep) {
+    if constexpr (PROBE) {
+      // readfirstlane waits for dep's VALU result, so the stamp follows the phase's work
+      const int sink = __builtin_amdgcn_readfirstlane(__double2hiint(dep));
+      const long long now = (long long)__builtin_amdgcn_s_memtime();
+      if (k >= 0) pr[k] += now - pt;
+      pr[7] += sink & 1;
+      pt = now;
+    }
+  };
   const int64_t i = blockIdx.x / np;
   const int p = (int)(blockIdx.x % np);
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int j = 64 * p + lane;
   const bool c1 = j < h1;
-  for (int k = 0; k < h0; ++k) sW2[k * 64 + lane] = c1 ? W2t[(int64_t)k * h1 + j] : 0.0;
-  constexpr int kU = kRollMaxH / 64;  // layer-1 columns per lane
-  double w1a[kU], w1b[kU], bb1[kU];
+  for (int k = wv; k < h0; k += kRollMwWaves)
+    sW2[k * 64 + lane] = c1 ? W2t[(int64_t)k * h1 + j] : 0.0;
+  // this wave's rows of the layer-2 sum (wave-uniform)
+  const int L = (h0 + kRollMwWaves - 1) / kRollMwWaves;
+  const int kb = min(wv * L, h0), len = min(kb + L, h0) - kb;
+  constexpr int kU1 = kRollMaxH / (64 * kRollMwWaves);  // layer-1 columns per thread
+  double w1a[kU1], w1b[kU1], bb1[kU1];
 #pragma unroll
-  for (int u = 0; u < kU; ++u) {
-    const int c = lane + 64 * u;
+  for (int u = 0; u < kU1; ++u) {
+    const int c = tid + 64 * kRollMwWaves * u;
     const bool ok = c < h0;
     w1a[u] = ok ? W1[2 * c] : 0.0;
     w1b[u] = ok ? W1[2 * c + 1] : 0.0;
     bb1[u] = ok ? b1[c] : 0.0;
   }
   const double bb2 = c1 ? b2[j] : 0.0;
-  double wm[kRollMaxA], sd[kRollMaxA], nz[kRollMaxA];
+  double wm[kRollMaxA], sd[kRollMaxA], nz[kRollMaxA], bmv[kRollMaxA];
 #pragma unroll
   for (int a = 0; a < kRollMaxA; ++a) {
     wm[a] = (c1 && a < a_dim) ? Wm[a * h1 + j] : 0.0;
+    bmv[a] = a < a_dim ? bm[a] : 0.0;
     sd[a] = a < a_dim ? exp(log_std[a]) : 0.0;
     nz[a] = a < a_dim ? noise[i * a_dim + a] : 0.0;
   }
-  // env state, stepped identically by every lane of every part of the trajectory
+  // env state, stepped identically by every thread of every part of the trajectory
   double pp = 0.0, vv = 0.0, x0, x1;
   float gx = 0.f, gy = 0.f;
   if (ENV == 0) {
@@ -345,101 +371,135 @@ __global__ __launch_bounds__(64) void rollout_mlp_mw_kernel(
     x0 = (double)gx;
     x1 = (double)gy;
   }
-  const bool rec = p == 0 && lane == 0;
+  const bool rec = p == 0 && tid == 0;
   if (rec) {
     states_rec[(i * (T + 1)) * 2 + 0] = (float)x0;
     states_rec[(i * (T + 1)) * 2 + 1] = (float)x1;
   }
+  if (tid == 0) sbad = 0;
   __syncthreads();
+  if constexpr (PROBE) pr[6] = -(long long)__builtin_amdgcn_s_memrealtime();
+  stamp(-1, 0.0);
   for (int64_t t = 0; t < T; ++t) {
     double nz_next[kRollMaxA];
     if (t + 1 < T)
       for (int a = 0; a < a_dim; ++a) nz_next[a] = noise[((t + 1) * n + i) * a_dim + a];
     // layer 1 (nf = 2), every column
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int c = lane + 64 * u;
+    for (int u = 0; u < kU1; ++u) {
+      const int c = tid + 64 * kRollMwWaves * u;
       if (c < h0)
         sh1[c] = fmax(__dadd_rn(__dadd_rn(__dmul_rn(x0, w1a[u]), __dmul_rn(x1, w1b[u])), bb1[u]),
                       0.0);
     }
     __syncthreads();
-    // layer 2, this part's columns: h2_j = relu(sum_k W2[j][k] h1[k] + b2[j]), k in order (one
-    // fma chain); the LDS operands of rows k+8 .. k+15 are loaded while rows k .. k+7 are summed
-    double acc = 0.0;
+    stamp(0, sh1[lane]);
+    // layer 2, this wave's rows of this part's columns: one fma chain in k order; the LDS
+    // operands of the next 8 rows are loaded while these 8 are summed (constant offsets from
+    // one base: no per-row address arithmetic)
     {
       constexpr int U = 8;
-      double wc[U], hc[U], wn[U], hn[U];
-      auto fetch = [&](double (&w)[U], double (&h)[U], int k0) {
+      const double* wp = sW2 + kb * 64 + lane;
+      const double* hp = sh1 + kb;
+      double acc = 0.0, wc[U], hc[U], wn[U], hn[U];
+      int k = 0;
+      if (len >= U) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int k = min(k0 + u, h0 - 1);  // clamped: rows past h0 are never summed
-          w[u] = sW2[k * 64 + lane];
-          h[u] = sh1[k];
+          wc[u] = wp[u * 64];
+          hc[u] = hp[u];
         }
-      };
-      fetch(wc, hc, 0);
-      int k = 0;
-      for (; k + U <= h0; k += U) {
-        fetch(wn, hn, k + U);
+        for (; k + 2 * U <= len; k += U) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            wn[u] = wp[(k + U + u) * 64];
+            hn[u] = hp[k + U + u];
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u) acc = fma(wc[u], hc[u], acc);
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            wc[u] = wn[u];
+            hc[u] = hn[u];
+          }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) acc = fma(wc[u], hc[u], acc);
+        k += U;
+      }
+      // the last < U rows: all loads issued, then the chain (one LDS round trip, not one per row)
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          wc[u] = wn[u];
-          hc[u] = hn[u];
+      for (int u = 0; u < U - 1; ++u)
+        if (k + u < len) {
+          wc[u] = wp[(k + u) * 64];
+          hc[u] = hp[k + u];
+        }
+#pragma unroll
+      for (int u = 0; u < U - 1; ++u)
+        if (k + u < len) acc = fma(wc[u], hc[u], acc);
+      spart[wv][lane] = acc;
+    }
+    __syncthreads();
+    unsigned long long* slot = mail + (i * T + t) * np * a_dim;
+    if (wv == 0) {
+      double s = spart[0][lane];
+#pragma unroll
+      for (int w = 1; w < kRollMwWaves; ++w) s += spart[w][lane];
+      const double h2 = c1 ? fmax(s + bb2, 0.0) : 0.0;
+      stamp(1, h2);
+      // mean layer: this part's partial over its 64 columns (xor shuffle tree), lane 0's, to
+      // this step's own mail words (pre-filled with kMailEmpty, which no partial can equal:
+      // each word validates itself, no flag)
+#pragma unroll
+      for (int a = 0; a < kRollMaxA; ++a) {
+        if (a < a_dim) {
+          double q = wm[a] * h2;
+#pragma unroll
+          for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m, kWave);
+          if (lane == 0)
+            __hip_atomic_store(slot + p * a_dim + a, __double_as_longlong(q), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         }
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (k + u < h0) acc = fma(wc[u], hc[u], acc);
-    }
-    const double h2 = c1 ? fmax(acc + bb2, 0.0) : 0.0;
-    // mean layer: this part's wave partial (the shuffle tree of rollout_mlp_kernel), lane 0's,
-    // published to this step's own mail words (8-B sc1 stores; every word is pre-filled with
-    // kMailEmpty, which no partial can equal, so each word validates itself: no flag, no wait)
-    unsigned long long* slot = mail + (i * T + t) * np * a_dim;
-#pragma unroll
-    for (int a = 0; a < kRollMaxA; ++a) {
-      if (a < a_dim) {
-        double q = wm[a] * h2;
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) q += __shfl_xor(q, m, kWave);
-        if (lane == 0)
-          __hip_atomic_store(slot + p * a_dim + a, __double_as_longlong(q), __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    // every part's partials of this step: lane l < np a_dim polls word l (part l / a_dim,
-    // action l % a_dim) with sc1 loads until it is published
-    double word = 0.0;
-    {
+      stamp(2, 0.0);
+      // every part's partials of this step: lane l < np a_dim polls word l (part l / a_dim,
+      // action l % a_dim) with sc1 loads until it is published
       const int nword = np * a_dim;
       unsigned spins = 0;
-      bool bad = false;
       unsigned long long v = 0;
       while (true) {
         if (lane < nword)
           v = __hip_atomic_load(slot + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!__ballot(lane < nword && v == kMailEmpty)) break;
         if (++spins > (1u << 24)) {
-          bad = true;
+          if (lane == 0) {
+            atomicExch(err, 1);
+            sbad = 1;
+          }
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      if (bad) {
-        if (lane == 0) atomicExch(err, 1);
-        return;
-      }
-      word = __longlong_as_double(v);
+      if constexpr (PROBE) pr[5] += spins;
+      sword[lane] = __longlong_as_double(v);
+      stamp(3, sword[lane]);
     }
+    __syncthreads();
+    if (sbad) return;  // workgroup-uniform: every wave leaves together
     double act[kRollMaxA];
     for (int a = 0; a < a_dim; ++a) {
-      double mu = __shfl(word, a, kWave);
-      for (int q = 1; q < np; ++q) mu += __shfl(word, q * a_dim + a, kWave);
+      // the parts' words loaded together, then summed in part order
+      constexpr int kMaxP = kRollMaxH / 64;
+      double wq[kMaxP];
+#pragma unroll
+      for (int q = 0; q < kMaxP; ++q)
+        if (q < np) wq[q] = sword[q * a_dim + a];
+      double mu = wq[0];
+#pragma unroll
+      for (int q = 1; q < kMaxP; ++q)
+        if (q < np) mu += wq[q];
       for (int q = np; q < nw; ++q) mu += 0.0;  // rollout_mlp_kernel's waves without columns
-      mu += bm[a];
+      mu += bmv[a];
       // output = mean + randn * exp(log_std)   (policy.py:59)
       act[a] = __dadd_rn(mu, __dmul_rn(nz[a], sd[a]));
       if (rec) actions_rec[(i * T + t) * a_dim + a] = (float)act[a];
@@ -463,11 +523,20 @@ __global__ __launch_bounds__(64) void rollout_mlp_mw_kernel(
         visited[(i * T + t) * 2 + 1] = x1;
       }
     }
-    __syncthreads();
+    stamp(4, x0);
   }
   if (rec && final_state) {
     final_state[2 * i] = x0;
     final_state[2 * i + 1] = x1;
+  }
+  if constexpr (PROBE) {
+    pr[6] += (long long)__builtin_amdgcn_s_memrealtime();
+    if (tid < 8) {
+      long long v = 0;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v = tid == k ? pr[k] : v;
+      probe[blockIdx.x * 8 + tid] = v;
+    }
   }
 }
 }  // namespace envs
@@ -526,7 +595,32 @@ static size_t rollout_mw_bytes(int64_t n, int64_t T, int h1, int a_dim) {
   const int64_t np = (h1 + 63) / 64;
   return 256 + (size_t)n * T * np * a_dim * 8;
 }
-static constexpr int kRollMwMaxH0 = 312;  // [h0][64] f64 slice + sh1 within 160 KB of LDS
+// [h0][64] f64 slice (dynamic) + sh1, spart, sword (static, 6.5 KB) within 160 KB of LDS
+static constexpr int kRollMwMaxH0 = 306;
+
+// the multi-workgroup form runs when every workgroup of every trajectory fits on the CUs at once
+static int rollout_use_mw(int64_t n, int h0, int h1, int a_dim) {
+  const int np = (h1 + 63) / 64;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 0;
+  const char* mw = getenv("MEPOL_ROLLOUT_MW");
+  return h0 <= kRollMwMaxH0 && n * np <= cus && np * a_dim <= 64 && !(mw && mw[0] == '0');
+}
+
+extern "C" int mepol_rollout_mlp_plan_info(int64_t n, int h0, int h1, int a_dim,
+                                           int* workgroups_per_traj, int* k_chunks) {
+  if (n <= 0 || h0 <= 0 || h1 <= 0 || h0 > kRollMaxH || h1 > kRollMaxH || a_dim <= 0 ||
+      a_dim > kRollMaxA || !workgroups_per_traj || !k_chunks) {
+    set_error("mepol_rollout_mlp_plan_info: bad arguments");
+    return kErrBadArg;
+  }
+  const int mw = rollout_use_mw(n, h0, h1, a_dim);
+  *workgroups_per_traj = mw ? (h1 + 63) / 64 : 1;
+  *k_chunks = mw ? kRollMwWaves : 1;
+  return 0;
+}
 
 extern "C" int mepol_rollout_mlp_workspace_size(int64_t n, int64_t T, int h0, int h1, int a_dim,
                                                 size_t* bytes) {
@@ -559,12 +653,8 @@ extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1,
   {
     // several workgroups per trajectory when all of them fit on the CUs at once
     const int np = (h1 + 63) / 64, nw = threads / 64;
-    int dev = 0, cus = 0;
-    MEPOL_HIP(hipGetDevice(&dev));
-    MEPOL_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const char* mw = getenv("MEPOL_ROLLOUT_MW");
     if (workspace && workspace_bytes >= rollout_mw_bytes(n, T, h1, a_dim) &&
-        h0 <= kRollMwMaxH0 && n * np <= cus && np * a_dim <= 64 && !(mw && mw[0] == '0')) {
+        rollout_use_mw(n, h0, h1, a_dim)) {
       char* ws = (char*)workspace;
       int* err = (int*)ws;
       unsigned long long* mail = (unsigned long long*)(ws + 256);
@@ -581,9 +671,10 @@ extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1,
                                     kRollMwMaxH0 * 64 * (int)sizeof(double)));                   \
       attr = true;                                                                               \
     }                                                                                            \
-    hipLaunchKernelGGL((rollout_mlp_mw_kernel<E>), dim3((unsigned)(n * np)), dim3(64), lds, st, \
+    hipLaunchKernelGGL((rollout_mlp_mw_kernel<E>), dim3((unsigned)(n * np)), dim3(256), lds, st,\
                        W1, b1, h0, W2t, b2, h1, Wm, bm, log_std, a_dim, init64, init32, noise, n, \
-                       T, states_rec, actions_rec, visited, final_state, np, nw, mail, err);     \
+                       T, states_rec, actions_rec, visited, final_state, np, nw, mail, err,      \
+                       nullptr);                                                                 \
   } while (0)
       if (env_id == 0)
         MEPOL_ROLL_MW(0);

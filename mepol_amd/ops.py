@@ -420,6 +420,16 @@ def rollout_mlp(env_id, W1, b1, W2, b2, Wm, bm, log_std, init, noise, states_rec
                          "(MEPOL_ROLLOUT_MW=0 selects the one-workgroup form)")
 
 
+def rollout_mlp_plan(n, h0, h1, a_dim):
+    """{"workgroups_per_traj", "k_chunks"}: the form mepol_rollout_mlp takes for this shape and
+    the layer-2 summation order it commits to (oracle.rollout_kordered's k_chunks)."""
+    import ctypes
+
+    wg, kc = ctypes.c_int(), ctypes.c_int()
+    call("mepol_rollout_mlp_plan_info", n, h0, h1, a_dim, ctypes.byref(wg), ctypes.byref(kc))
+    return {"workgroups_per_traj": wg.value, "k_chunks": kc.value}
+
+
 def memcpy_async(dst, src):
     """dst <- src (same byte size; device or pinned host tensors), ordered on the current
     stream; inside a graph capture this is a memcpy node."""

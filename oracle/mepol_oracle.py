@@ -242,16 +242,17 @@ def _native():
                             "-lm"], check=True)
         lib = ctypes.CDLL(so)
         vp, i64, ci = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
-        lib.rollout_kordered.argtypes = [ci, i64, i64, ci, ci, ci] + [vp] * 12
+        lib.rollout_kordered.argtypes = [ci, i64, i64, ci, ci, ci, ci] + [vp] * 12
         lib.rollout_kordered.restype = ci
         _NATIVE["lib"] = lib
     return _NATIVE["lib"]
 
 
-def rollout_kordered(env, sd, std, init, noise, T):
+def rollout_kordered(env, sd, std, init, noise, T, k_chunks=1):
     """collect_particles (mepol.py:76-109) for the 2 -> [h0, h1] -> a ReLU policy with the MLP
     summed in the documented k-ordered / butterfly order of oracle/native/rollout_kordered.c
-    (the order the HIP rollout kernels commit to), so actions compare bit for bit.
+    (the order the HIP rollout kernels commit to), so actions compare bit for bit; k_chunks =
+    the k-ranges of the second layer's sum (ops.rollout_mlp_plan reports the kernel's).
     std: exp(log_std) [a] f64; init [nt, 2] (f64 MountainCar, f32 GridWorld); noise [T, nt, a].
     Returns states f32 [nt, T+1, 2], actions f32 [nt, T, a]."""
     def arr(x, dt):
@@ -270,7 +271,8 @@ def rollout_kordered(env, sd, std, init, noise, T):
     states = np.zeros((nt, T + 1, 2), np.float32)
     actions = np.zeros((nt, T, a_dim), np.float32)
     p = lambda x: None if x is None else x.ctypes.data  # noqa: E731
-    rc = _native().rollout_kordered(0 if mc else 1, nt, T, h0, h1, a_dim, p(W1), p(b1), p(W2),
+    rc = _native().rollout_kordered(0 if mc else 1, nt, T, h0, h1, a_dim, int(k_chunks), p(W1),
+                                    p(b1), p(W2),
                                     p(b2), p(Wm), p(bm), p(sdv), p(i64), p(i32), p(nz),
                                     p(states), p(actions))
     assert rc == 0

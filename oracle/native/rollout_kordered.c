@@ -8,7 +8,9 @@
  * rollout kernels (mepol_amd/csrc/envs.hip) commit to, so their actions can be compared bit for
  * bit instead of to ~1e-15:
  *   h1_c  = max((x0 * W1[c][0] + x1 * W1[c][1]) + b1[c], 0)         each op rounded
- *   h2_j  = max(fma-chain_k(W2[j][k] * h1_k, k = 0 .. h0-1) + b2[j], 0)
+ *   h2_j  = max(((c_0 + c_1) + ...) + b2[j], 0),  c_r = fma-chain_k(W2[j][k] * h1_k) over
+ *           k in [r L, min(r L + L, h0)), L = ceil(h0 / k_chunks), r = 0 .. k_chunks - 1
+ *           (k_chunks = 1: one chain over all rows; the multi-workgroup kernel uses 4)
  *   part_w[a] = xor-butterfly sum (strides 32, 16, .., 1; lane 0's value) of Wm[a][j] * h2_j over
  *               the 64 columns j of wave w (zero past h1), w = 0 .. ceil(max(h0,h1)/64) - 1
  *   mu[a] = ((part_0 + part_1) + ...) + bm[a];  a = mu + noise * sd   (policy.py:59)
@@ -55,13 +57,20 @@ static void gw_step(float* sx, float* sy, double ax, double ay) {
 }
 
 /* mean [a_dim] of one state in the order above */
-static void mlp_mean(double x0, double x1, int h0, int h1, int a_dim, const double* W1,
+static void mlp_mean(double x0, double x1, int h0, int h1, int a_dim, int k_chunks,
+                     const double* W1,
                      const double* b1, const double* W2, const double* b2, const double* Wm,
                      const double* bm, double* hid1, double* hid2, double* mu) {
   for (int c = 0; c < h0; ++c) hid1[c] = fmax((x0 * W1[2 * c] + x1 * W1[2 * c + 1]) + b1[c], 0.0);
   for (int j = 0; j < h1; ++j) {
+    const int L = (h0 + k_chunks - 1) / k_chunks;
     double acc = 0.0;
-    for (int k = 0; k < h0; ++k) acc = fma(W2[(int64_t)j * h0 + k], hid1[k], acc);
+    for (int r = 0; r < k_chunks; ++r) {
+      const int kb = r * L < h0 ? r * L : h0, ke = kb + L < h0 ? kb + L : h0;
+      double c = 0.0;
+      for (int k = kb; k < ke; ++k) c = fma(W2[(int64_t)j * h0 + k], hid1[k], c);
+      acc = (r == 0) ? c : acc + c;
+    }
     hid2[j] = fmax(acc + b2[j], 0.0);
   }
   const int hmax = h0 > h1 ? h0 : h1;
@@ -87,11 +96,12 @@ static void mlp_mean(double x0, double x1, int h0, int h1, int a_dim, const doub
 
 /* env 0 = MountainCar (init64 [n][2]), 1 = GridWorld (init32 [n][2]); noise [T][n][a_dim];
  * W2 [h1][h0] (nn.Linear layout); states [n][T+1][2] f32, actions [n][T][a_dim] f32. */
-int rollout_kordered(int env, int64_t n, int64_t T, int h0, int h1, int a_dim, const double* W1,
+int rollout_kordered(int env, int64_t n, int64_t T, int h0, int h1, int a_dim, int k_chunks,
+                     const double* W1,
                      const double* b1, const double* W2, const double* b2, const double* Wm,
                      const double* bm, const double* sd, const double* init64,
                      const float* init32, const double* noise, float* states, float* actions) {
-  if (a_dim > 8 || h0 <= 0 || h1 <= 0) return 1;
+  if (a_dim > 8 || h0 <= 0 || h1 <= 0 || k_chunks <= 0) return 1;
   double* hid1 = (double*)malloc(sizeof(double) * h0);
   double* hid2 = (double*)malloc(sizeof(double) * h1);
   for (int64_t i = 0; i < n; ++i) {
@@ -112,7 +122,7 @@ int rollout_kordered(int env, int64_t n, int64_t T, int h0, int h1, int a_dim, c
     states[(i * (T + 1)) * 2 + 1] = (float)x1;
     for (int64_t t = 0; t < T; ++t) {
       double mu[8], act[8];
-      mlp_mean(x0, x1, h0, h1, a_dim, W1, b1, W2, b2, Wm, bm, hid1, hid2, mu);
+      mlp_mean(x0, x1, h0, h1, a_dim, k_chunks, W1, b1, W2, b2, Wm, bm, hid1, hid2, mu);
       for (int a = 0; a < a_dim; ++a) {
         act[a] = mu[a] + noise[(t * n + i) * a_dim + a] * sd[a];
         actions[(i * T + t) * a_dim + a] = (float)act[a];

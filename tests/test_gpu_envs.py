@@ -190,7 +190,8 @@ def test_rollout_mlp_bitexact_vs_kordered_oracle(cuda, monkeypatch, env, mw, hid
     actions are bit-identical and so are the GridWorld states (f32 state, f64 move: no
     transcendental); MountainCar's cos() may round differently from glibc in the last ulp, so
     its states / actions are checked to 1e-12.  Both kernel forms (ceil(h1/64) workgroups per
-    trajectory, MEPOL_ROLLOUT_MW=1, and one workgroup per trajectory) give the same bits."""
+    trajectory, MEPOL_ROLLOUT_MW=1, and one workgroup per trajectory) match the oracle in the
+    summation order they report (ops.rollout_mlp_plan: k_chunks)."""
     from mepol_amd import ops
     from mepol_amd.policy import GaussianPolicy
 
@@ -209,7 +210,10 @@ def test_rollout_mlp_bitexact_vs_kordered_oracle(cuda, monkeypatch, env, mw, hid
     # exp(log_std) as the device computes it (ocml); it agrees with numpy's to an ulp
     std_dev = torch.exp(pol.log_std.detach()).cpu().numpy()
     np.testing.assert_allclose(std_dev, np.exp(sd["log_std"]), rtol=2.3e-16, atol=0)
-    S_ref, A_ref = O.rollout_kordered(env, sd, std_dev, init, noise, T)
+    plan = ops.rollout_mlp_plan(nt, hidden[0], hidden[1], a_dim)
+    assert plan["workgroups_per_traj"] == (1 if mw == "0" or hidden[0] > 306 else
+                                           (hidden[1] + 63) // 64)
+    S_ref, A_ref = O.rollout_kordered(env, sd, std_dev, init, noise, T, plan["k_chunks"])
     dev = "cuda"
     states = torch.zeros((nt, T + 1, 2), dtype=torch.float32, device=dev)
     actions = torch.zeros((nt, T, a_dim), dtype=torch.float32, device=dev)

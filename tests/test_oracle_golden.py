@@ -149,3 +149,30 @@ def test_env_steps_oracle():
     np.testing.assert_allclose(O.mountaincar_step(z["S"], z["A"]), z["NS"], rtol=0, atol=1e-15)
     z = load_golden("env_gw")
     assert np.array_equal(O.gridworld_step(z["S"], z["A"]), z["NS"])
+
+
+@pytest.mark.parametrize("env", ["mountaincar", "gridworld"])
+@pytest.mark.parametrize("k_chunks", [1, 4])
+def test_rollout_kordered_matches_rollout_oracle(env, k_chunks):
+    """The k-ordered C restatement (the order the HIP rollout kernels commit to, one or four
+    k-ranges in the second layer) agrees with the numpy restatement of collect_particles to
+    rounding: the same f32 actions and states up to a last-place flip over a short horizon."""
+    rng = np.random.default_rng(k_chunks)
+    h0, h1, a_dim = 300, 300, (1 if env == "mountaincar" else 2)
+    sd = {"net.0.weight": rng.standard_normal((h0, 2)) * 0.5, "net.0.bias": rng.standard_normal(h0) * 0.1,
+          "net.2.weight": rng.standard_normal((h1, h0)) / h0 ** 0.5,
+          "net.2.bias": rng.standard_normal(h1) * 0.1,
+          "mean.weight": rng.standard_normal((a_dim, h1)) / h1 ** 0.5,
+          "mean.bias": rng.standard_normal(a_dim) * 0.1}
+    log_std = np.full(a_dim, -1.0)
+    nt, T = 6, 25
+    if env == "mountaincar":
+        init = np.stack([rng.uniform(-0.6, -0.4, nt), np.zeros(nt)], 1)
+    else:
+        init = rng.uniform(-6, -4, (nt, 2)).astype(np.float32)
+    noise = rng.standard_normal((T, nt, a_dim))
+    S0, A0 = O.rollout(env, sd, log_std, init, noise, T)
+    S1, A1 = O.rollout_kordered(env, sd, np.exp(log_std), init, noise, T, k_chunks)
+    np.testing.assert_allclose(A1, A0, rtol=0, atol=1e-5)   # f32 actions of the same f64 means
+    np.testing.assert_allclose(S1, S0, rtol=0, atol=1e-5)
+    assert np.mean(A1 == A0) > 0.9
