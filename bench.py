@@ -380,7 +380,9 @@ def run(args):
 
     if rank != 0:
         if dist is not None:
-            dist.destroy_process_group()
+            from mepol_amd import parallel
+
+            parallel.destroy_process_group(dist)
         return
 
     from mepol_amd import parallel
@@ -462,7 +464,7 @@ def run(args):
         line["cpu_baseline"] = cpu_baseline(cfg, args.cpu_sample_queries, iters_done)
     _emit(line)
     if dist is not None:
-        dist.destroy_process_group()
+        parallel.destroy_process_group(dist)
 
 
 PEAK_F64_TFLOPS = 78.6            # MI355X spec: FP64 matrix (dense)

@@ -31,6 +31,10 @@
 extern "C" {
 #endif
 
+/* Bumped on every incompatible change of the signatures below (2: mepol_rollout_mlp takes a
+ * workspace; mepol_gemm_dpp removed).  mepol_abi_version() returns the library's value. */
+#define MEPOL_ABI_VERSION 2
+
 #define MEPOL_ERR_BAD_ARG 1001
 #define MEPOL_ERR_WORKSPACE 1002
 #define MEPOL_ERR_UNSUPPORTED 1003

@@ -16,6 +16,8 @@ _c_dbl = ctypes.c_double
 _c_sz = ctypes.c_size_t
 _c_vp = ctypes.c_void_p
 
+ABI_VERSION = 2  # include/mepol_amd.h MEPOL_ABI_VERSION
+
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 SIGNATURES = {
     "mepol_last_error_string": [],
@@ -103,6 +105,10 @@ def load():
                 fn = getattr(lib, name)
                 fn.argtypes = argtypes
                 fn.restype = _RESTYPES.get(name, ctypes.c_int)
+            got = lib.mepol_abi_version()
+            if got != ABI_VERSION:
+                raise MepolError(f"{LIB_PATH} has C ABI version {got}, this binding expects "
+                                 f"{ABI_VERSION}: rebuild the library (make)")
             _lib = lib
     return _lib
 

@@ -91,7 +91,9 @@ class DeviceIteration:
     """Static buffers + captured graph for one (policy, optimizer, batch shape, k, constants)."""
 
     def __init__(self, target_policy, optimizer, batch, k, G, B, ns, eps):
-        self.tgt, self.opt = target_policy, optimizer
+        # the cache below is keyed weakly by the target policy: a strong reference here would
+        # keep every iteration (its graphs and ~1 GB of static buffers at C3) alive for good
+        self._tgt_ref, self.opt = weakref.ref(target_policy), optimizer
         self.kind = _opt_kind(optimizer)
         self.params = list(target_policy.parameters())  # optimizer / state order
         l1, l2 = [m for m in target_policy.net if isinstance(m, nn.Linear)]
@@ -150,6 +152,10 @@ class DeviceIteration:
         self.s_gemm = torch.cuda.Stream(device=dev)
         self._batch_id = None
         self._init_state()
+
+    @property
+    def tgt(self):
+        return self._tgt_ref()
 
     def matches(self, target_policy, optimizer, batch, k, G, B, ns, eps):
         return (target_policy is self.tgt and optimizer is self.opt and batch.N == self.N
@@ -410,7 +416,10 @@ class DeviceIteration:
         for par in range(len(self._bufs)):
             self._use(par)
             graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph, stream=self._side):
+            # thread-local capture: a capture in "global" mode makes other threads' HIP calls
+            # fail, and ProcessGroupNCCL's watchdog thread queries the events of earlier eager
+            # collectives at any time (an error there aborts the process)
+            with torch.cuda.graph(graph, stream=self._side, capture_error_mode="thread_local"):
                 self._body()
             graphs.append(graph)
         cur.wait_stream(self._side)
@@ -464,6 +473,17 @@ class DeviceIteration:
             torch._foreach_copy_(self.params, self._bufs[par]["shadow"])
             torch._foreach_add_([self.opt.state[p]["step"] for p in self.params], -1.0)
             self._next = par
+
+
+    def release(self):
+        """Wait for replays in flight and free the captured graphs (before the process group
+        whose collectives a sharded graph captured is destroyed)."""
+        if self._inflight:
+            self.cancel()
+        for g in self.graphs:
+            if g is not None:
+                g.reset()
+        self.graph = None
 
 
 _CACHE = weakref.WeakKeyDictionary()  # target policy -> DeviceIteration

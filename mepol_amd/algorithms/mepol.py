@@ -73,7 +73,7 @@ class _RolloutGraph:
             self._body(1)
         torch.cuda.current_stream().wait_stream(side)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=side):
+        with torch.cuda.graph(self.graph, stream=side, capture_error_mode="thread_local"):
             self._body(T)
         torch.cuda.current_stream().wait_stream(side)
 
@@ -386,13 +386,24 @@ def compute_importance_weights(behavioral_policy, target_policy, states, actions
     return _IWFunction.apply(logp_t, logp_b, batch)
 
 
-def compute_entropy(behavioral_policy, target_policy, states, actions, num_traj, real_traj_lengths,
-                    distances, indices, k, G, B, ns, eps):
-    """KL (Kozachenko-Leonenko) entropy estimate, 0-d f64 (mepol.py:142-154)."""
+def _entropy_device(behavioral_policy, target_policy, states, actions, num_traj,
+                    real_traj_lengths, distances, indices, k, G, B, ns, eps):
+    """compute_entropy's estimate left on the device (no host synchronisation)."""
     batch = P.lookup(states, actions, real_traj_lengths, distances, indices)
     logp_t, logp_b = _logps(batch, behavioral_policy, target_policy)
     H, _ = _EntropyFunction.apply(logp_t, logp_b, batch, k, G, B, ns, eps)
     return H
+
+
+def compute_entropy(behavioral_policy, target_policy, states, actions, num_traj, real_traj_lengths,
+                    distances, indices, k, G, B, ns, eps):
+    """KL (Kozachenko-Leonenko) entropy estimate, 0-d f64 (mepol.py:142-154).
+
+    Returned on the host, as the reference's CPU computation returns it: its caller reads it
+    with .numpy() (mepol.py:367-368, 497-498).  The copy is differentiable, so
+    ``(-compute_entropy(...)).backward()`` reaches the target policy's parameters on the GPU."""
+    return _entropy_device(behavioral_policy, target_policy, states, actions, num_traj,
+                           real_traj_lengths, distances, indices, k, G, B, ns, eps).cpu()
 
 
 def compute_kl_deferred(behavioral_policy, target_policy, states, actions, num_traj,
@@ -426,7 +437,7 @@ def compute_kl(behavioral_policy, target_policy, states, actions, num_traj, real
     """
     kl, flag = compute_kl_deferred(behavioral_policy, target_policy, states, actions, num_traj,
                                    real_traj_lengths, distances, indices, k, eps)
-    return kl, bool(flag)
+    return kl.cpu(), bool(flag)  # host tensor, as the reference's (its caller: kl.numpy(), :439)
 
 
 def policy_update_deferred(optimizer, behavioral_policy, target_policy, states, actions, num_traj,
@@ -434,7 +445,7 @@ def policy_update_deferred(optimizer, behavioral_policy, target_policy, states, 
     """policy_update with the numeric-error flag (taken on the loss before backward, as at
     mepol.py:274-276) left on the device as a 0-d bool tensor."""
     optimizer.zero_grad()
-    loss = -compute_entropy(behavioral_policy, target_policy, states, actions, num_traj, traj_len,
+    loss = -_entropy_device(behavioral_policy, target_policy, states, actions, num_traj, traj_len,
                             distances, indices, k, G, B, ns, eps)
     flag = ~torch.isfinite(loss.detach())
     loss.backward()
@@ -452,7 +463,8 @@ def policy_update(optimizer, behavioral_policy, target_policy, states, actions, 
     loss, flag = policy_update_deferred(optimizer, behavioral_policy, target_policy, states,
                                         actions, num_traj, traj_len, distances, indices, k, G, B,
                                         ns, eps)
-    return loss, bool(flag)
+    # host tensor, as the reference's (its caller: -loss.detach().numpy(), mepol.py:432)
+    return loss.detach().cpu(), bool(flag)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -16,7 +16,7 @@ void set_error(const char* fmt, ...) {
 
 extern "C" const char* mepol_last_error_string(void) { return mepol::g_err; }
 
-extern "C" int mepol_abi_version(void) { return 1; }
+extern "C" int mepol_abi_version(void) { return MEPOL_ABI_VERSION; }
 
 // Stream-ordered copy between device and (pinned) host buffers; under stream capture it becomes
 // a memcpy node, so a replayed graph can read its scalar inputs from and write its control

@@ -135,17 +135,22 @@ __global__ void rollout_step_kernel(double* __restrict__ env_f64, float* __restr
 // reference's 2-hidden-layer ReLU policy: x -> relu(W1 x + b1) -> relu(W2 h1 + b2) -> mean
 // (policy.py:21-28, 53-61) -> a = mean + noise * exp(log_std) -> env step, with the states /
 // actions recorded as f32.  Thread j owns hidden column j; its W1 row, biases and mean-layer
-// column stay in registers, the first KR rows of W2^T (k-major, [h0][h1]) too, and the rest of
-// W2^T streams from L2 each step (coalesced: one 8-byte word per thread per k).  Replaces the
-// per-step launch sequence (3 GEMMs + bias/ReLU + rollout_step, ~58 us per step even as a
+// column stay in registers, the first KL rows of W2^T (k-major, [h0][h1]) in LDS, and the rest
+// of W2^T streams from L2 each step (coalesced: one 8-byte word per thread per k).  Replaces
+// the per-step launch sequence (3 GEMMs + bias/ReLU + rollout_step, ~58 us per step even as a
 // replayed graph) with ~3 barriers per step.
+// Summation order: the layer-2 sum runs as kRollChunks fma chains over the row ranges
+// [r L, r L + L), L = ceil(h0 / kRollChunks), combined as ((c0 + c1) + c2) + c3 -- exactly the
+// multi-workgroup form's order (one chain per wave there), so both forms give the same bits
+// and the host may pick either (or fall back from one to the other) per call.
 constexpr int kRollMaxH = 512;
 // mail word not yet published (memset 0xff): a NaN bit pattern no f64 partial sum of the
 // policy's finite weights and activations produces
 constexpr unsigned long long kMailEmpty = ~0ull;
 constexpr int kRollMaxA = 8;
+constexpr int kRollChunks = 4;
 
-template <int ENV, int KR, int U>
+template <int ENV, int U>
 __global__ __launch_bounds__(kRollMaxH) void rollout_mlp_kernel(
     const double* __restrict__ W1, const double* __restrict__ b1, int h0,
     const double* __restrict__ W2t, const double* __restrict__ b2, int h1,
@@ -154,7 +159,7 @@ __global__ __launch_bounds__(kRollMaxH) void rollout_mlp_kernel(
     const float* __restrict__ init32, const double* __restrict__ noise, int64_t n, int64_t T,
     float* __restrict__ states_rec, float* __restrict__ actions_rec,
     double* __restrict__ visited, double* __restrict__ final_state, int KL) {
-  extern __shared__ double sW2[];  // [KL][blockDim.x]: W2^T rows KR .. KR + KL - 1
+  extern __shared__ double sW2[];  // [KL][blockDim.x]: W2^T rows 0 .. KL - 1
   __shared__ double sx[2];
   __shared__ double sh1[kRollMaxH];
   __shared__ double spart[kRollMaxH / 64][kRollMaxA];
@@ -166,10 +171,8 @@ __global__ __launch_bounds__(kRollMaxH) void rollout_mlp_kernel(
   double wm[kRollMaxA];
 #pragma unroll
   for (int a = 0; a < kRollMaxA; ++a) wm[a] = (c1 && a < a_dim) ? Wm[a * h1 + j] : 0.0;
-  double w2r[KR > 0 ? KR : 1];
-#pragma unroll
-  for (int k = 0; k < KR; ++k) w2r[k] = (c1 && k < h0) ? W2t[(int64_t)k * h1 + j] : 0.0;
-  for (int k = 0; k < KL; ++k) sW2[k * blockDim.x + j] = c1 ? W2t[(int64_t)(KR + k) * h1 + j] : 0.0;
+  for (int k = 0; k < KL; ++k) sW2[k * blockDim.x + j] = c1 ? W2t[(int64_t)k * h1 + j] : 0.0;
+  const int L = (h0 + kRollChunks - 1) / kRollChunks;
   double p = 0.0, v = 0.0;  // MountainCar state (thread 0)
   float gx = 0.f, gy = 0.f;  // GridWorld state (thread 0)
   if (j == 0) {
@@ -197,6 +200,7 @@ __global__ __launch_bounds__(kRollMaxH) void rollout_mlp_kernel(
     }
   }
   __syncthreads();
+  const double* col = W2t + (c1 ? j : 0);
   for (int64_t t = 0; t < T; ++t) {
     double nz_next[kRollMaxA];
     if (j == 0 && t + 1 < T)
@@ -205,19 +209,17 @@ __global__ __launch_bounds__(kRollMaxH) void rollout_mlp_kernel(
     if (c0) sh1[j] = fmax(__dadd_rn(__dadd_rn(__dmul_rn(sx[0], w1a), __dmul_rn(sx[1], w1b)), bb1),
                           0.0);
     __syncthreads();
-    // layer 2: h2_j = relu(sum_k W2[j][k] h1[k] + b2[j]), k in order
+    // layer 2: h2_j = relu(sum_r c_r + b2[j]), c_r the fma chain over rows [r L, r L + L) in k
+    // order; rows below KL come from LDS, the rest stream from L2 in batches of U loads with the
+    // next batch in flight while this one is summed (L2 latency-bound: U rows per round trip)
     double acc = 0.0;
-#pragma unroll
-    for (int k = 0; k < KR; ++k) acc = fma(w2r[k], sh1[k], acc);
-    for (int k = 0; k < KL; ++k) acc = fma(sW2[k * blockDim.x + j], sh1[KR + k], acc);
-    {
-      // streamed rows: batches of U loads, the next batch in flight while this one is summed
-      // (L2 latency-bound: U rows per round trip)
-      const double* col = W2t + (c1 ? j : 0);
-      const int k0 = KR + KL;
-      int k = k0;
+    for (int r = 0; r < kRollChunks; ++r) {
+      const int ka = min(r * L, h0), kb = min(ka + L, h0);
+      double c = 0.0;
+      int k = ka;
+      for (; k < min(kb, KL); ++k) c = fma(sW2[k * blockDim.x + j], sh1[k], c);
       double cur[U], nxt[U];
-      const int kend = k0 + ((h0 - k0) / U) * U;
+      const int kend = k + ((kb - k) / U) * U;
       if (k < kend) {
 #pragma unroll
         for (int u = 0; u < U; ++u) cur[u] = col[(int64_t)(k + u) * h1];
@@ -227,12 +229,13 @@ __global__ __launch_bounds__(kRollMaxH) void rollout_mlp_kernel(
             for (int u = 0; u < U; ++u) nxt[u] = col[(int64_t)(k + U + u) * h1];
           }
 #pragma unroll
-          for (int u = 0; u < U; ++u) acc = fma(c1 ? cur[u] : 0.0, sh1[k + u], acc);
+          for (int u = 0; u < U; ++u) c = fma(c1 ? cur[u] : 0.0, sh1[k + u], c);
 #pragma unroll
           for (int u = 0; u < U; ++u) cur[u] = nxt[u];
         }
       }
-      for (; k < h0; ++k) acc = fma(c1 ? col[(int64_t)k * h1] : 0.0, sh1[k], acc);
+      for (; k < kb; ++k) c = fma(c1 ? col[(int64_t)k * h1] : 0.0, sh1[k], c);
+      acc = r == 0 ? c : acc + c;
     }
     const double h2 = c1 ? fmax(acc + bb2, 0.0) : 0.0;
     // mean layer: per-wave partial sums over its 64 columns, then waves in order
@@ -301,7 +304,7 @@ __global__ __launch_bounds__(kRollMaxH) void rollout_mlp_kernel(
 // launches it only when n * NP <= the CU count.
 // PROBE (tools/variants/rollout_probe.hip only): thread 0 of each workgroup accumulates
 // s_memtime spans of the step's phases into probe[blockIdx.x][8]; the product has PROBE = false.
-constexpr int kRollMwWaves = 4;
+constexpr int kRollMwWaves = kRollChunks;  // one layer-2 chain per wave
 template <int ENV, bool PROBE = false>
 __global__ __launch_bounds__(64 * kRollMwWaves) void rollout_mlp_mw_kernel(
     const double* __restrict__ W1, const double* __restrict__ b1, int h0,
@@ -590,7 +593,8 @@ extern "C" int mepol_rollout_step(int env_id, double* env_f64, float* env_f32, c
 // nf = 2 -> [h0, h1] -> a_dim with ReLU: W1 [h0,2], b1, W2t = W2^T [h0,h1], b2, Wm [a,h1], bm,
 // log_std [a]; noise [T,n,a_dim] f64.  Writes states_rec [n,T+1,2] f32, actions_rec [n,T,a] f32,
 // visited [n,T,2] f64 (nullable), final_state [n,2] f64 (nullable).
-// Multi-workgroup form: err (word 0), then mail [n][T][np][a_dim] 8-byte words (kMailEmpty).
+// Workspace: word 0 = error flag (zeroed by every call that gets a workspace), then for the
+// multi-workgroup form the mail [n][T][np][a_dim] 8-byte words (kMailEmpty).
 static size_t rollout_mw_bytes(int64_t n, int64_t T, int h1, int a_dim) {
   const int64_t np = (h1 + 63) / 64;
   return 256 + (size_t)n * T * np * a_dim * 8;
@@ -598,15 +602,51 @@ static size_t rollout_mw_bytes(int64_t n, int64_t T, int h1, int a_dim) {
 // [h0][64] f64 slice (dynamic) + sh1, spart, sword (static, 6.5 KB) within 160 KB of LDS
 static constexpr int kRollMwMaxH0 = 306;
 
-// the multi-workgroup form runs when every workgroup of every trajectory fits on the CUs at once
-static int rollout_use_mw(int64_t n, int h0, int h1, int a_dim) {
+template <int ENV>
+static int rollout_mw_prepare() {
+  static bool attr = false;
+  if (!attr) {
+    MEPOL_HIP(hipFuncSetAttribute((const void*)rollout_mlp_mw_kernel<ENV>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  kRollMwMaxH0 * 64 * (int)sizeof(double)));
+    attr = true;
+  }
+  return 0;
+}
+
+// The multi-workgroup form needs every workgroup of a trajectory resident at once (its parts
+// exchange partial sums every step).  It is launched as a COOPERATIVE kernel, whose contract
+// is exactly that (all workgroups co-resident, or the launch fails), and only when the
+// occupancy of the kernel at this LDS size times the CU count holds the whole grid; otherwise
+// (and when the cooperative launch is refused) the one-workgroup form runs, which sums in the
+// same order and so gives the same bits.
+static int rollout_use_mw(int env_id, int64_t n, int h0, int h1, int a_dim) {
   const int np = (h1 + 63) / 64;
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-    return 0;
   const char* mw = getenv("MEPOL_ROLLOUT_MW");
-  return h0 <= kRollMwMaxH0 && n * np <= cus && np * a_dim <= 64 && !(mw && mw[0] == '0');
+  if (h0 > kRollMwMaxH0 || np * a_dim > 64 || (mw && mw[0] == '0')) return 0;
+  int dev = 0, cus = 0, coop = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess ||
+      !coop)
+    return 0;
+  const size_t lds = (size_t)h0 * 64 * sizeof(double);
+  int per_cu = 0;
+  hipError_t e;
+  if (env_id == 0) {
+    if (rollout_mw_prepare<0>()) return 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rollout_mlp_mw_kernel<0>,
+                                                     64 * kRollMwWaves, lds);
+  } else {
+    if (rollout_mw_prepare<1>()) return 0;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, rollout_mlp_mw_kernel<1>,
+                                                     64 * kRollMwWaves, lds);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n * np <= (int64_t)per_cu * cus;
 }
 
 extern "C" int mepol_rollout_mlp_plan_info(int64_t n, int h0, int h1, int a_dim,
@@ -616,9 +656,10 @@ extern "C" int mepol_rollout_mlp_plan_info(int64_t n, int h0, int h1, int a_dim,
     set_error("mepol_rollout_mlp_plan_info: bad arguments");
     return kErrBadArg;
   }
-  const int mw = rollout_use_mw(n, h0, h1, a_dim);
+  // (GridWorld and MountainCar kernels have the same resources: env 1 stands for both)
+  const int mw = rollout_use_mw(1, n, h0, h1, a_dim);
   *workgroups_per_traj = mw ? (h1 + 63) / 64 : 1;
-  *k_chunks = mw ? kRollMwWaves : 1;
+  *k_chunks = kRollChunks;  // both forms
   return 0;
 }
 
@@ -628,8 +669,31 @@ extern "C" int mepol_rollout_mlp_workspace_size(int64_t n, int64_t T, int h0, in
     set_error("mepol_rollout_mlp_workspace_size: bad arguments");
     return kErrBadArg;
   }
-  *bytes = rollout_mw_bytes(n, T, h1, a_dim);
+  // the mail only when the multi-workgroup form would run; the error word always
+  *bytes = (n > 0 && rollout_use_mw(1, n, h0, h1, a_dim)) ? rollout_mw_bytes(n, T, h1, a_dim)
+                                                          : 256;
   return 0;
+}
+
+template <int ENV>
+static hipError_t rollout_mw_launch(const double* W1, const double* b1, int h0,
+                                    const double* W2t, const double* b2, int h1, const double* Wm,
+                                    const double* bm, const double* log_std, int a_dim,
+                                    const double* init64, const float* init32,
+                                    const double* noise, int64_t n, int64_t T, float* states_rec,
+                                    float* actions_rec, double* visited, double* final_state,
+                                    int np, int nw, unsigned long long* mail, int* err,
+                                    hipStream_t st) {
+  long long* probe = nullptr;
+  void* args[] = {(void*)&W1,         (void*)&b1,          (void*)&h0,      (void*)&W2t,
+                  (void*)&b2,         (void*)&h1,          (void*)&Wm,      (void*)&bm,
+                  (void*)&log_std,    (void*)&a_dim,       (void*)&init64,  (void*)&init32,
+                  (void*)&noise,      (void*)&n,           (void*)&T,       (void*)&states_rec,
+                  (void*)&actions_rec, (void*)&visited,    (void*)&final_state, (void*)&np,
+                  (void*)&nw,         (void*)&mail,        (void*)&err,     (void*)&probe};
+  return hipLaunchCooperativeKernel((const void*)rollout_mlp_mw_kernel<ENV>,
+                                    dim3((unsigned)(n * np)), dim3(64 * kRollMwWaves), args,
+                                    (unsigned)((size_t)h0 * 64 * sizeof(double)), st);
 }
 
 extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1, int h0,
@@ -643,80 +707,63 @@ extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1,
   if (h0 <= 0 || h1 <= 0 || h0 > kRollMaxH || h1 > kRollMaxH || a_dim <= 0 ||
       a_dim > kRollMaxA || env_id < 0 || env_id > 1 || (env_id == 0 && !init64) ||
       (env_id == 1 && (!init32 || a_dim != 2)) || !W1 || !b1 || !W2t || !b2 || !Wm || !bm ||
-      !log_std || !noise || !states_rec || !actions_rec) {
+      !log_std || !noise || !states_rec || !actions_rec ||
+      (workspace && workspace_bytes < sizeof(int))) {
     set_error("mepol_rollout_mlp: bad arguments (hidden <= %d, a_dim <= %d)", kRollMaxH,
               kRollMaxA);
     return kErrBadArg;
   }
   const int threads = ((h0 > h1 ? h0 : h1) + 63) / 64 * 64;
   hipStream_t st = (hipStream_t)stream;
+  int* err = (int*)workspace;
+  if (err) MEPOL_HIP(hipMemsetAsync(err, 0, sizeof(int), st));  // whichever form runs
   {
-    // several workgroups per trajectory when all of them fit on the CUs at once
+    // several workgroups per trajectory when all of them can be resident at once
     const int np = (h1 + 63) / 64, nw = threads / 64;
     if (workspace && workspace_bytes >= rollout_mw_bytes(n, T, h1, a_dim) &&
-        rollout_use_mw(n, h0, h1, a_dim)) {
-      char* ws = (char*)workspace;
-      int* err = (int*)ws;
-      unsigned long long* mail = (unsigned long long*)(ws + 256);
-      MEPOL_HIP(hipMemsetAsync(err, 0, sizeof(int), st));
+        rollout_use_mw(env_id, n, h0, h1, a_dim)) {
+      unsigned long long* mail = (unsigned long long*)((char*)workspace + 256);
       // every mail word starts as kMailEmpty (all ones)
       MEPOL_HIP(hipMemsetAsync(mail, 0xff, (size_t)n * T * np * a_dim * 8, st));
-      const size_t lds = (size_t)h0 * 64 * sizeof(double);
-#define MEPOL_ROLL_MW(E)                                                                         \
-  do {                                                                                           \
-    static bool attr = false;                                                                    \
-    if (!attr) {                                                                                 \
-      MEPOL_HIP(hipFuncSetAttribute((const void*)rollout_mlp_mw_kernel<E>,                       \
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,                  \
-                                    kRollMwMaxH0 * 64 * (int)sizeof(double)));                   \
-      attr = true;                                                                               \
-    }                                                                                            \
-    hipLaunchKernelGGL((rollout_mlp_mw_kernel<E>), dim3((unsigned)(n * np)), dim3(256), lds, st,\
-                       W1, b1, h0, W2t, b2, h1, Wm, bm, log_std, a_dim, init64, init32, noise, n, \
-                       T, states_rec, actions_rec, visited, final_state, np, nw, mail, err,      \
-                       nullptr);                                                                 \
-  } while (0)
-      if (env_id == 0)
-        MEPOL_ROLL_MW(0);
-      else
-        MEPOL_ROLL_MW(1);
-#undef MEPOL_ROLL_MW
-      MEPOL_CHECK_LAUNCH();
-      return 0;
+      const hipError_t e =
+          env_id == 0
+              ? rollout_mw_launch<0>(W1, b1, h0, W2t, b2, h1, Wm, bm, log_std, a_dim, init64,
+                                     init32, noise, n, T, states_rec, actions_rec, visited,
+                                     final_state, np, nw, mail, err, st)
+              : rollout_mw_launch<1>(W1, b1, h0, W2t, b2, h1, Wm, bm, log_std, a_dim, init64,
+                                     init32, noise, n, T, states_rec, actions_rec, visited,
+                                     final_state, np, nw, mail, err, st);
+      if (e == hipSuccess) return 0;
+      (void)hipGetLastError();  // refused (e.g. hipErrorCooperativeLaunchTooLarge): one-wg form
     }
   }
   const dim3 g((unsigned)n);
-  const char* kr = getenv("MEPOL_ROLLOUT_KR");
-  const int want = kr ? atoi(kr) : 0;
-  const int kr_used = want >= 32 ? 32 : 0;
-  // W2^T rows kept in LDS after the register rows: up to ~150 KB (MEPOL_ROLLOUT_KL caps it)
+  // W2^T rows kept in LDS, the rest streamed: up to ~150 KB (MEPOL_ROLLOUT_KL caps it)
   const char* klv = getenv("MEPOL_ROLLOUT_KL");
   int KL = (int)((150 * 1024) / ((size_t)threads * sizeof(double)));
   if (klv) KL = std::min(KL, atoi(klv));
-  KL = std::max(0, std::min(KL, h0 - kr_used));
+  KL = std::max(0, std::min(KL, h0));
   const size_t lds = (size_t)KL * threads * sizeof(double);
   const char* uv = getenv("MEPOL_ROLLOUT_U");
   const int u = uv ? atoi(uv) : 8;
-#define MEPOL_ROLL(E, KR, U)                                                                      \
+#define MEPOL_ROLL(E, U)                                                                          \
   do {                                                                                            \
     static bool attr = false;                                                                     \
     if (!attr) {                                                                                  \
-      MEPOL_HIP(hipFuncSetAttribute((const void*)rollout_mlp_kernel<E, KR, U>,                    \
+      MEPOL_HIP(hipFuncSetAttribute((const void*)rollout_mlp_kernel<E, U>,                        \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));     \
       attr = true;                                                                                \
     }                                                                                             \
-    hipLaunchKernelGGL((rollout_mlp_kernel<E, KR, U>), g, dim3(threads), lds, st, W1, b1, h0, W2t, \
-                       b2, h1, Wm, bm, log_std, a_dim, init64, init32, noise, n, T, states_rec,   \
+    hipLaunchKernelGGL((rollout_mlp_kernel<E, U>), g, dim3(threads), lds, st, W1, b1, h0, W2t, b2, \
+                       h1, Wm, bm, log_std, a_dim, init64, init32, noise, n, T, states_rec,       \
                        actions_rec, visited, final_state, KL);                                    \
   } while (0)
   if (env_id == 0) {
-    if (kr_used >= 32) MEPOL_ROLL(0, 32, 8);
-    else if (u >= 16) MEPOL_ROLL(0, 0, 16);
-    else MEPOL_ROLL(0, 0, 8);
+    if (u >= 16) MEPOL_ROLL(0, 16);
+    else MEPOL_ROLL(0, 8);
   } else {
-    if (kr_used >= 32) MEPOL_ROLL(1, 32, 8);
-    else if (u >= 16) MEPOL_ROLL(1, 0, 16);
-    else MEPOL_ROLL(1, 0, 8);
+    if (u >= 16) MEPOL_ROLL(1, 16);
+    else MEPOL_ROLL(1, 8);
   }
 #undef MEPOL_ROLL
   MEPOL_CHECK_LAUNCH();

@@ -127,7 +127,8 @@ def main(argv=None):
         ndev = torch.cuda.device_count()
         local = int(os.environ.get("LOCAL_RANK", "0")) % ndev
         torch.cuda.set_device(local)
-        if not dist.is_initialized():
+        dist_owned = not dist.is_initialized()
+        if dist_owned:
             if ndev >= world:
                 from ..parallel import prepare_nccl_env
 
@@ -195,6 +196,10 @@ def main(argv=None):
           num_workers=args.num_workers)
     if dist is not None:
         dist.barrier()
+        if dist_owned:
+            from ..parallel import destroy_process_group
+
+            destroy_process_group(dist)
     return 0
 
 

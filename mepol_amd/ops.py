@@ -410,14 +410,20 @@ def rollout_mlp(env_id, W1, b1, W2, b2, Wm, bm, log_std, init, noise, states_rec
     nbytes = ctypes.c_size_t()
     call("mepol_rollout_mlp_workspace_size", n, T, h0, h1, a_dim, ctypes.byref(nbytes))
     ws = _workspace(init.device, nbytes.value, tag="rollout")
-    call("mepol_rollout_mlp", env_id, ptr(W1.contiguous()), ptr(b1), h0, ptr(W2t), ptr(b2), h1,
-         ptr(Wm.contiguous()), ptr(bm), ptr(log_std.contiguous()), a_dim, ptr(init64), ptr(init32),
-         ptr(noise.contiguous()), n, T, ptr(states_rec), ptr(actions_rec), ptr(visited), None,
-         ptr(ws), ws.numel(), _stream())
-    # word 0: the multi-workgroup form's flag (its workgroups could not all run at once)
+    args = (env_id, ptr(W1.contiguous()), ptr(b1), h0, ptr(W2t), ptr(b2), h1,
+            ptr(Wm.contiguous()), ptr(bm), ptr(log_std.contiguous()), a_dim, ptr(init64),
+            ptr(init32), ptr(noise.contiguous()), n, T, ptr(states_rec), ptr(actions_rec),
+            ptr(visited), None)
+    call("mepol_rollout_mlp", *args, ptr(ws), ws.numel(), _stream())
+    # word 0 (zeroed by the call): the multi-workgroup form gave up waiting for a part of a
+    # trajectory.  The one-workgroup form (no workspace) sums in the same order and rewrites
+    # every output, so the result is the same bits either way.
     if int(ws[:4].view(torch.int32)[0].item()) != 0:
-        raise _lib.MepolError("mepol_rollout_mlp: the workgroups of a trajectory were not co-resident "
-                         "(MEPOL_ROLLOUT_MW=0 selects the one-workgroup form)")
+        import warnings
+
+        warnings.warn("mepol_rollout_mlp: workgroups of a trajectory were not co-resident; "
+                      "re-ran the one-workgroup form")
+        call("mepol_rollout_mlp", *args, None, 0, _stream())
 
 
 def rollout_mlp_plan(n, h0, h1, a_dim):

@@ -39,6 +39,30 @@ def prepare_nccl_env():
     os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
 
 
+def release_graphs():
+    """Free every captured sharded iteration.  Its graphs hold RCCL collectives recorded on the
+    process group's communicator: they must be gone (and nothing of theirs in flight) before
+    that communicator is torn down, or RCCL's threads meet a destroyed communicator."""
+    its = list(_SHARDED_CACHE.values())
+    if its:
+        torch.cuda.synchronize()
+        for it in its:
+            it.release()
+        torch.cuda.synchronize()
+    _SHARDED_CACHE.clear()
+    _GRAPH_STATE.clear()
+
+
+def destroy_process_group(dist, group=None):
+    """release_graphs(), then dist.destroy_process_group(group): the teardown every caller of
+    the sharded path uses (CLI, bench, tests)."""
+    release_graphs()
+    if group is None:
+        dist.destroy_process_group()
+    else:
+        dist.destroy_process_group(group)
+
+
 class ShardedEpoch:
     def __init__(self, states, actions, real_traj_lengths, next_states_f32, k, dist, group=None,
                  ops=None):
@@ -244,6 +268,16 @@ class ShardedEpoch:
         if not DL.supported(view, beh, tgt, optimizer) or _GRAPH_STATE.get("disabled"):
             return None
         if self.dist.get_backend(self.group) != "nccl":  # only RCCL collectives can be captured
+            return None
+        if os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") != "0":
+            # the group recycles events across capture and eager use (prepare_nccl_env): a
+            # captured graph would put the watchdog thread at risk, so stay eager
+            if not _GRAPH_STATE.get("warned"):
+                import warnings
+
+                warnings.warn("sharded iteration runs eagerly: call parallel.prepare_nccl_env() "
+                              "before init_process_group('nccl') to enable graph replay")
+                _GRAPH_STATE["warned"] = True
             return None
         it = _SHARDED_CACHE.get(tgt)
         if it is None or not it.matches_epoch(tgt, optimizer, self, G, B, ns, eps):

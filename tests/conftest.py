@@ -14,6 +14,13 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X) and the built HIP library")
 
 
+def pytest_runtest_logstart(nodeid, location):
+    """Name every test on stderr before it runs: if a native thread aborts the process, the
+    last line of the log says which test was running."""
+    sys.stderr.write(f"[mepol-test] start {nodeid}\n")
+    sys.stderr.flush()
+
+
 def load_golden(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
 

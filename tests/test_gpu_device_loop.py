@@ -195,17 +195,27 @@ def _two_epochs(monkeypatch, graph):
             s = torch.randn(3 * NT * T, NF, dtype=torch.float64, device="cuda")
             a = torch.randn(3 * NT * T, A, dtype=torch.float64, device="cuda")
             big.get_log_p(s, a).sum().backward()
+    from mepol_amd.algorithms import device_loop
+
     params = torch.cat([p.detach().reshape(-1) for p in last.parameters()]).cpu().numpy()
-    return out, params
+    import weakref
+
+    return out, params, (tgt in device_loop._CACHE, weakref.ref(tgt))
 
 
 def test_graph_scratch_survives_eager_growth(cuda, monkeypatch):
     """a captured iteration must not write through scratch the eager path replaced."""
     from mepol_amd.algorithms import device_loop
 
-    g_out, g_params = _two_epochs(monkeypatch, True)
-    assert len(device_loop._CACHE) >= 1
-    e_out, e_params = _two_epochs(monkeypatch, False)
+    g_out, g_params, (used, tgt_ref) = _two_epochs(monkeypatch, True)
+    assert used
+    # the cache is keyed weakly by the target policy and its entry does not keep it alive:
+    # once the caller's policy is gone, so is the graph with its ~N-sized static buffers
+    import gc
+
+    gc.collect()
+    assert tgt_ref() is None
+    e_out, e_params, _ = _two_epochs(monkeypatch, False)
     np.testing.assert_allclose(g_out, e_out, rtol=1e-9)
     np.testing.assert_allclose(g_params, e_params, rtol=1e-8, atol=1e-11)
 

@@ -142,16 +142,18 @@ def test_rollout_graph_and_shards_match_eager(cuda, monkeypatch, env_name, fused
 
 
 @pytest.mark.parametrize("env", ["mountaincar", "gridworld"])
-@pytest.mark.parametrize("kr", ["0", "32", "64"])
-def test_rollout_mlp_kernel_matches_oracle(cuda, monkeypatch, env, kr):
-    """The one-launch rollout (mepol_rollout_mlp: policy MLP + noise + env step for all T steps,
-    one workgroup per trajectory) == the oracle's per-step rollout with the same injected noise,
-    to the rounding of the MLP's summation order; the register-cached W2 rows (MEPOL_ROLLOUT_KR)
-    do not change the result."""
+@pytest.mark.parametrize("kl", ["0", "37", "300"])
+def test_rollout_mlp_kernel_matches_oracle(cuda, monkeypatch, env, kl):
+    """The one-launch rollout, one workgroup per trajectory (mepol_rollout_mlp: policy MLP +
+    noise + env step for all T steps) == the oracle's per-step rollout with the same injected
+    noise to the rounding of the MLP's summation order, and == the k-ordered oracle (4 chunks)
+    bit for bit; how many W2 rows sit in LDS rather than stream from L2 (MEPOL_ROLLOUT_KL,
+    37 = a chunk boundary inside the LDS rows) does not change the result."""
     from mepol_amd import ops
     from mepol_amd.policy import GaussianPolicy
 
-    monkeypatch.setenv("MEPOL_ROLLOUT_KR", kr)
+    monkeypatch.setenv("MEPOL_ROLLOUT_KL", kl)
+    monkeypatch.setenv("MEPOL_ROLLOUT_MW", "0")
     torch.manual_seed(5)
     a_dim = 1 if env == "mountaincar" else 2
     pol = GaussianPolicy([300, 300], 2, a_dim, -0.5 if env == "mountaincar" else -1.5).cuda()
@@ -164,6 +166,8 @@ def test_rollout_mlp_kernel_matches_oracle(cuda, monkeypatch, env, kr):
     noise = rng.standard_normal((T, nt, a_dim))
     sd = {k: v.detach().cpu().numpy() for k, v in pol.state_dict().items()}
     S_ref, A_ref = O.rollout(env, sd, sd["log_std"], init, noise, T)
+    std_dev = torch.exp(pol.log_std.detach()).cpu().numpy()
+    S_ko, A_ko = O.rollout_kordered(env, sd, std_dev, init, noise, T, 4)
     dev = "cuda"
     states = torch.zeros((nt, T + 1, 2), dtype=torch.float32, device=dev)
     actions = torch.zeros((nt, T, a_dim), dtype=torch.float32, device=dev)
@@ -179,6 +183,99 @@ def test_rollout_mlp_kernel_matches_oracle(cuda, monkeypatch, env, kr):
     assert (S == S_ref).mean() > 0.99
     assert np.abs(S - S_ref).max() < 1e-3
     assert np.array_equal(visited.cpu().numpy().astype(np.float32), S[:, 1:])
+    if env == "gridworld":
+        assert np.array_equal(A, A_ko) and np.array_equal(S, S_ko)
+    else:
+        np.testing.assert_allclose(A, A_ko, rtol=0, atol=1e-12)
+
+
+def _rollout_inputs(env, hidden, nt, T, seed):
+    from mepol_amd.policy import GaussianPolicy
+
+    torch.manual_seed(seed)
+    a_dim = 1 if env == "mountaincar" else 2
+    pol = GaussianPolicy(hidden, 2, a_dim, -0.5 if env == "mountaincar" else -1.5).cuda()
+    rng = np.random.default_rng(seed)
+    if env == "mountaincar":
+        init = np.stack([rng.uniform(-0.6, -0.4, nt), np.zeros(nt)], 1)
+    else:
+        init = rng.uniform(-6, -4, (nt, 2)).astype(np.float32)
+    noise = rng.standard_normal((T, nt, a_dim))
+    return pol, init, noise
+
+
+def _rollout_run(env, pol, init, noise):
+    from mepol_amd import ops
+
+    T, nt, a_dim = noise.shape
+    states = torch.zeros((nt, T + 1, 2), dtype=torch.float32, device="cuda")
+    actions = torch.zeros((nt, T, a_dim), dtype=torch.float32, device="cuda")
+    l1, l2 = pol.net[0], pol.net[2]
+    ops.rollout_mlp(0 if env == "mountaincar" else 1, l1.weight.detach(), l1.bias.detach(),
+                    l2.weight.detach(), l2.bias.detach(), pol.mean.weight.detach(),
+                    pol.mean.bias.detach(), pol.log_std.detach(),
+                    torch.as_tensor(init, device="cuda"),
+                    torch.as_tensor(noise, dtype=torch.float64, device="cuda"), states, actions)
+    return states, actions
+
+
+@pytest.mark.parametrize("env", ["mountaincar", "gridworld"])
+@pytest.mark.parametrize("hidden", [[300, 300], [64, 48], [400, 300], [2, 130]])
+def test_rollout_forms_bit_identical(cuda, monkeypatch, env, hidden):
+    """Both forms of mepol_rollout_mlp sum layer 2 in the same 4-chunk order: several
+    workgroups per trajectory (MEPOL_ROLLOUT_MW=1) and one (=0) give the same bits, so the host
+    may pick either per call (a rank's shard and the one-rank batch can take different forms)."""
+    from mepol_amd import ops
+
+    pol, init, noise = _rollout_inputs(env, hidden, 24, 50, 9)
+    monkeypatch.setenv("MEPOL_ROLLOUT_MW", "1")
+    plan = ops.rollout_mlp_plan(24, hidden[0], hidden[1], noise.shape[2])
+    assert plan["k_chunks"] == 4
+    assert plan["workgroups_per_traj"] == (1 if hidden[0] > 306 else (hidden[1] + 63) // 64)
+    s1, a1 = _rollout_run(env, pol, init, noise)
+    monkeypatch.setenv("MEPOL_ROLLOUT_MW", "0")
+    assert ops.rollout_mlp_plan(24, hidden[0], hidden[1], noise.shape[2])["workgroups_per_traj"] == 1
+    s0, a0 = _rollout_run(env, pol, init, noise)
+    assert torch.equal(a1, a0) and torch.equal(s1, s0)
+
+
+def test_rollout_error_word_reset(cuda, monkeypatch):
+    """the error word of a reused rollout workspace is zeroed by every call, whichever
+    form runs -- a workspace full of 0xff (a stale flag) must not raise."""
+    from mepol_amd import ops
+
+    pol, init, noise = _rollout_inputs("gridworld", [300, 300], 8, 20, 2)
+    ref = _rollout_run("gridworld", pol, init, noise)
+    for mw in ("0", "1"):
+        monkeypatch.setenv("MEPOL_ROLLOUT_MW", mw)
+        ops._workspace(torch.device("cuda", 0), 1 << 20, tag="rollout").fill_(0xFF)
+        out = _rollout_run("gridworld", pol, init, noise)
+        assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
+
+
+def test_rollout_under_concurrent_load(cuda, monkeypatch):
+    """the multi-workgroup rollout must not depend on having the CUs to itself.  A
+    long f64 GEMM queue occupies every CU from another stream while the rollout is launched; the
+    result must be the same bits as on an idle GPU (cooperative launch, or the one-workgroup
+    fallback, which sums in the same order), with no co-residency error."""
+    import warnings
+
+    monkeypatch.setenv("MEPOL_ROLLOUT_MW", "1")
+    pol, init, noise = _rollout_inputs("gridworld", [300, 300], 20, 400, 4)
+    ref = _rollout_run("gridworld", pol, init, noise)
+    a = torch.randn(4096, 4096, dtype=torch.float64, device="cuda")
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    with warnings.catch_warnings():
+        warnings.simplefilter("error")  # a co-residency fallback warning fails the test
+        with torch.cuda.stream(side):
+            for _ in range(12):  # ~3 ms each: the queue outlasts the rollout's launch
+                b = a @ a
+        out = _rollout_run("gridworld", pol, init, noise)
+        torch.cuda.synchronize()
+    del b
+    assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
 
 
 @pytest.mark.parametrize("env", ["mountaincar", "gridworld"])

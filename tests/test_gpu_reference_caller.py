@@ -1,0 +1,110 @@
+"""The function-level drop-in (VERDICT r3 "what's missing" #2): the build's
+collect_particles_and_compute_knn / compute_entropy / policy_update / compute_kl driven by a
+caller shaped like the reference's own epoch (src/algorithms/mepol.py:347-368 and :404-499),
+including every ``.numpy()`` it applies to their results (:367-368, :432, :439, :497-498).
+
+The loop below is written for this test: the reference's control flow (accept while the KL is
+below the threshold, backtracking with lr0 / coeff^i, at most one step after a backtrack, stop
+at max_off_iters, final entropy of the last valid target), with the module's functions swapped
+in one by one.  It must run unchanged and take the same decisions, entropies and KLs as the
+build's own graph-replayed off_policy_optimization on the same particles."""
+import copy
+
+import numpy as np
+import pytest
+import scipy.special
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _reference_shaped_epoch(M, env, beh, tgt, last_valid, optimizer, num_traj, traj_len, k,
+                            kl_threshold, max_off_iters, backtrack_coeff, max_backtrack_try,
+                            lr0, ns, eps):
+    B = np.log(k) - scipy.special.digamma(k)
+    G = scipy.special.gamma(ns / 2 + 1)
+    states, actions, real_traj_lengths, next_states, distances, indices = \
+        M.collect_particles_and_compute_knn(env, beh, num_traj, traj_len, None, k, 1)
+    with torch.no_grad():
+        entropy = M.compute_entropy(beh, beh, states, actions, num_traj, real_traj_lengths,
+                                    distances, indices, k, G, B, ns, eps)
+    entropy0 = entropy.numpy()                                     # mepol.py:368
+    trace = []
+    last_valid.load_state_dict(tgt.state_dict())
+    num_off_iters, backtrack_iter, learning_rate = 0, 1, lr0
+    for g in optimizer.param_groups:
+        g["lr"] = learning_rate
+    done = False
+    while not done:
+        loss, numeric_error = M.policy_update(optimizer, beh, tgt, states, actions, num_traj,
+                                              real_traj_lengths, distances, indices, k, G, B, ns,
+                                              eps)
+        entropy = -loss.detach().numpy()                           # mepol.py:432
+        with torch.no_grad():
+            kl, kl_numeric_error = M.compute_kl(beh, tgt, states, actions, num_traj,
+                                                real_traj_lengths, distances, indices, k, eps)
+        kl = kl.numpy()                                            # mepol.py:439
+        if not numeric_error and not kl_numeric_error and kl <= kl_threshold:
+            last_valid.load_state_dict(tgt.state_dict())
+            num_off_iters += 1
+            trace.append((num_off_iters, float(entropy), float(kl), learning_rate))
+        else:
+            if backtrack_iter != max_backtrack_try:
+                tgt.load_state_dict(last_valid.state_dict())
+                learning_rate = lr0 / (backtrack_coeff ** backtrack_iter)
+                for g in optimizer.param_groups:
+                    g["lr"] = learning_rate
+                backtrack_iter += 1
+                continue
+            done = True
+        if backtrack_iter > 1 or num_off_iters == max_off_iters:
+            done = True
+    with torch.no_grad():
+        entropy = M.compute_entropy(last_valid, last_valid, states, actions, num_traj,
+                                    real_traj_lengths, distances, indices, k, G, B, ns, eps)
+    assert not (torch.isnan(entropy) or torch.isinf(entropy))
+    final = entropy.numpy()                                        # mepol.py:497-498
+    return dict(entropy0=float(entropy0), trace=trace, final=float(final),
+                n=num_off_iters, bt=backtrack_iter, lr=learning_rate,
+                batch=(states, actions, real_traj_lengths, distances, indices, G, B))
+
+
+@pytest.mark.parametrize("kl_threshold,lr", [(2.0, 1e-3), (0.02, 3e-2)])
+def test_reference_shaped_epoch_matches_graph_loop(cuda, kl_threshold, lr):
+    from mepol_amd.algorithms import mepol as M
+    from mepol_amd.envs import ErgodicEnv, GridWorldContinuous
+    from mepol_amd.policy import GaussianPolicy
+
+    k, nt, T, ns, eps = 10, 8, 400, 2, 0.0
+    env = ErgodicEnv(GridWorldContinuous())
+    torch.manual_seed(2)
+    beh = GaussianPolicy([300, 300], 2, 2, -1.5).cuda()
+    tgt = copy.deepcopy(beh)
+    last = copy.deepcopy(beh)
+    init = copy.deepcopy(beh.state_dict())
+    opt = torch.optim.Adam(tgt.parameters(), lr=lr)
+    torch.manual_seed(5)  # the rollout's noise
+    ref = _reference_shaped_epoch(M, env, beh, tgt, last, opt, nt, T, k, kl_threshold, 6, 2, 4,
+                                  lr, ns, eps)
+    # the returned scalars are host tensors, as the reference's (its caller calls .numpy())
+    st, ac, rl, D, I, G, B = ref["batch"]
+    with torch.no_grad():
+        h = M.compute_entropy(beh, beh, st, ac, nt, rl, D, I, k, G, B, ns, eps)
+    assert h.device.type == "cpu" and h.dtype == torch.float64 and h.dim() == 0
+    assert ref["n"] >= 1
+
+    # the build's own loop (graph replay + speculation) on the same particles
+    beh.load_state_dict(init)
+    tgt.load_state_dict(init)
+    last.load_state_dict(init)
+    opt = torch.optim.Adam(tgt.parameters(), lr=lr)
+    trace = []
+    H, n, bt, lr_out = M.off_policy_optimization(
+        opt, beh, tgt, last, st, ac, nt, rl, D, I, k, G, B, ns, eps, kl_threshold, 6, True, 2, 4,
+        lr, on_accept=lambda i, e, kl, l: trace.append((i, float(e), float(kl), l)))
+    assert (n, bt, lr_out) == (ref["n"], ref["bt"], ref["lr"])
+    assert len(trace) == len(ref["trace"])
+    for a, b in zip(trace, ref["trace"]):
+        assert a[0] == b[0] and a[3] == b[3]
+        np.testing.assert_allclose(a[1:3], b[1:3], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(float(M._np(H)), ref["final"], rtol=1e-9)
