@@ -15,13 +15,17 @@ all: $(LIB) $(ORACLE_NATIVE)
 $(ORACLE_NATIVE): oracle/native/rollout_kordered.c
 	gcc -O2 -ffp-contract=off -fPIC -shared $< -o $@ -lm
 
-build/%.o: mepol_amd/csrc/%.hip mepol_amd/csrc/common.hpp include/mepol_amd.h
+build/%.o: mepol_amd/csrc/%.hip $(wildcard mepol_amd/csrc/*.hpp) include/mepol_amd.h
 	@mkdir -p build
 	$(HIPCC) $(FLAGS) $(FLAGS_$*) -Iinclude -c $< -o $@
 
 # k-NN selection compares finite MFMA outputs (inputs are validated first): no NaN
 # canonicalisation before v_min; MFMA results in VGPRs (no accvgpr copies per tile)
 FLAGS_knn := -fno-honor-nans -mllvm -amdgpu-mfma-vgpr-form
+FLAGS_knn_select_ks1 := $(FLAGS_knn)
+FLAGS_knn_select_ks2 := $(FLAGS_knn)
+FLAGS_knn_select_ks3 := $(FLAGS_knn)
+FLAGS_knn_select_ks4 := $(FLAGS_knn)
 
 $(LIB): $(OBJ)
 	$(HIPCC) $(FLAGS) -shared -o $@ $(OBJ)

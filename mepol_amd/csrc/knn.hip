@@ -25,87 +25,10 @@
 //                queued.
 //   4. exact   : queued queries are answered by an exhaustive f64 scan (no approximation),
 //                a handful of queries spread over the whole grid (chunked scan + merge).
-#include "common.hpp"
-
-#include <algorithm>
-#include <cfloat>
-#include <climits>
-#include <cmath>
-#include <cstdlib>
+#include "knn_common.hpp"
 
 namespace mepol {
 namespace knn {
-
-using f32x16 = __attribute__((ext_vector_type(16))) float;
-using f32x4 = __attribute__((ext_vector_type(4))) float;
-using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
-
-constexpr int kBufCap = 24;        // per-lane LDS insertion buffer (entries)
-constexpr int kMaxSplit = 16;
-constexpr int kExactGrid = 512;    // blocks of the exhaustive fallback (exact_kernel)
-constexpr int kRefineList = 64;    // approximate candidates refine ranks per query (one wave)
-
-// ---------------------------------------------------------------------------------------
-// 2. select: list helpers
-// ---------------------------------------------------------------------------------------
-template <int LIST>
-__device__ __forceinline__ void list_insert(float (&ld)[LIST], int (&li)[LIST], float x, int xi) {
-  // ld ascending; precondition x < ld[LIST-1].  Branch-free shift-insert.
-  bool c[LIST];
-#pragma unroll
-  for (int j = 0; j < LIST; ++j) c[j] = x < ld[j];
-#pragma unroll
-  for (int j = LIST - 1; j >= 1; --j) {
-    ld[j] = c[j - 1] ? ld[j - 1] : (c[j] ? x : ld[j]);
-    li[j] = c[j - 1] ? li[j - 1] : (c[j] ? xi : li[j]);
-  }
-  ld[0] = c[0] ? x : ld[0];
-  li[0] = c[0] ? xi : li[0];
-}
-
-// Merge this lane's LDS buffer into its sorted list; then share the prune bound with the
-// partner lane (l ^ 32 serves the same query column).  Every lane of the wave calls it.
-// keep > 0 (split-f16 select): the bound also takes max(own keep-th, partner's keep-th): the
-// two half lists then hold >= 2 keep values at or below it, so 2 keep >= kp1 + slack of the
-// query's candidates in this range are never pruned; this bound is far tighter than a list's
-// own last entry (the LIST-th of one half).  The bound only decreases over the scan.
-template <int LIST>
-__device__ __forceinline__ float list_at(const float (&ld)[LIST], int j) {
-  float v = INFINITY;
-#pragma unroll
-  for (int i = 0; i < LIST; ++i) v = (i == j) ? ld[i] : v;
-  return v;
-}
-
-template <int LIST>
-__device__ __forceinline__ void flush_buffer(float (&ld)[LIST], int (&li)[LIST], float& thr, int& cnt,
-                                             const float (*bv)[64], const int (*bi)[64], int l,
-                                             float thr0, int keep = 0) {
-  const int mc = wave_max_i(cnt);
-#pragma nounroll
-  for (int e = 0; e < mc; ++e) {
-    if (e < cnt) {
-      const float x = bv[e][l];
-      const int xi = bi[e][l];
-      if (x < thr) {
-        list_insert<LIST>(ld, li, x, xi);
-        thr = ld[LIST - 1];
-      }
-    }
-  }
-  cnt = 0;
-  // lanes l and l^32 serve the same query: the tighter of their maxima is a valid prune bound
-  // for both (refine's certification bound is the min over all lanes' final bounds and the
-  // query's sampled bound thr0).
-  thr = fminf(thr0, fminf(ld[LIST - 1], __shfl_xor(ld[LIST - 1], 32, kWave)));
-  if (keep > 0) {
-    const float kv = list_at<LIST>(ld, keep - 1);
-    thr = fminf(thr, fmaxf(kv, __shfl_xor(kv, 32, kWave)));
-  }
-}
-
-// Row (candidate within the tile) of accumulator register r for lane l (32x32 C/D map).
-__device__ __forceinline__ int acc_row(int r, int l) { return (r & 3) + 8 * (r >> 2) + 4 * (l >> 5); }
 
 // ---------------------------------------------------------------------------------------
 // 0./1. input check, scale and pack
@@ -148,24 +71,6 @@ __global__ __launch_bounds__(256) void norms_kernel(const float* __restrict__ X,
     if (b2) atomicAdd(bad + 1, (unsigned)__popcll(b2));
   }
 }
-
-// sigma = 2^e with sigma * max(cmax, qmax) in (64, 128] (1 when the data is all zero).
-__device__ __forceinline__ float knn_scale(const unsigned* __restrict__ scal) {
-  const float m = fmaxf(__uint_as_float(scal[0]), __uint_as_float(scal[2]));
-  // slack for the f32 rounding of sqrt in norms_kernel: 127.9 instead of 128
-  if (!(m > 0.f) || !(m < 3e38f)) return 1.f;
-  int e;
-  (void)frexpf(127.9f / m, &e);
-  e = max(-100, min(100, e - 1));
-  return ldexpf(1.f, e);
-}
-
-__device__ __forceinline__ void split_f16(float v, _Float16& hi, _Float16& lo) {
-  hi = (_Float16)v;
-  lo = (_Float16)(v - (float)hi);  // v - hi is exact in f32
-}
-
-constexpr float kPadNorm16 = 60000.f;  // scaled |c|^2 of padding candidates (> any real D')
 
 // apack16[((t*64 + l)*KS16 + s)*16 + {0..7 hi, 8..15 lo}] = A[i = l&31][k = 16 s + 8 (l>>5) + j]
 // of candidate tile t: f<d: -2 sigma x_cf ; f==d: |sigma c|^2 ; else 0.
@@ -225,240 +130,6 @@ __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X
     }
     *reinterpret_cast<f16x8*>(apack + (((t * KS16 + s) * nh) * 64 + l) * 8) = hv;
     if (nh == 2) *reinterpret_cast<f16x8*>(apack + (((t * KS16 + s) * 2 + 1) * 64 + l) * 8) = lv;
-  }
-}
-
-// Partial top-LIST lists of every query over its split's tile range.  The queries are split into
-// f16 hi + lo (2^-22 relative).  NH = 1 (candidate-hi, the default): the candidates are the f16
-// hi halves of A and 2 MFMAs per k-step (A_hi q_hi + A_hi q_lo) accumulate in f32; the value's
-// error is dominated by the candidate rounding, 2^-11 (|c|^2 + 2 |c||q|), and only the hi half
-// travels (1 KB per k-step and tile).  NH = 2 (split candidates): A_hi and A_lo travel and 3
-// MFMAs per k-step (+ A_lo q_hi) give ~f32-class values, 2 (3 K + 16 + d) 2^-24 (|c|^2 + 2 |c||q|),
-// for data whose neighbour spacing is below the f16 band (make_plan).  refine's certification
-// uses the plan's bound either way.
-// OCC = 3: __launch_bounds__(256, 3) caps the kernel at 168 VGPRs (3 waves per SIMD) for the
-// short-list instances (a few spilled dwords, on the insertion path only).
-template <int KS16, int LIST, int NH, int OCC>
-__global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __restrict__ apack,
-                                                       const float* __restrict__ query,
-                                                       int64_t nq, int d, int64_t nct, int split,
-                                                       int64_t tiles_per_split, int keep,
-                                                       const unsigned* __restrict__ scal,
-                                                       float* __restrict__ out_v,
-                                                       int* __restrict__ out_i) {
-  __shared__ float sbuf_v[4][kBufCap][64];
-  __shared__ int sbuf_i[4][kBufCap][64];
-  const int w = threadIdx.x >> 6;
-  const int l = threadIdx.x & 63;
-  // XCD-aware block mapping: workgroups go round-robin over the 8 XCDs by linear id, so with
-  // sp = id % split (split a multiple of 8) every XCD only ever reads the candidate ranges
-  // sp = xcd (mod 8), which then stay resident in that XCD's 4 MB L2.  Any other split (2 at
-  // C3) keeps the split-major order: the blocks in flight then all read one candidate range.
-  const int64_t lin = (int64_t)blockIdx.x + (int64_t)blockIdx.y * gridDim.x;
-  const bool xcd_map = (split & 7) == 0;
-  const int sp = xcd_map ? (int)(lin % split) : (int)blockIdx.y;
-  const int64_t qt = (xcd_map ? lin / split : (int64_t)blockIdx.x) * 4 + w;
-  if (qt * 32 >= nq) return;  // wave-uniform
-  const int h = l >> 5;
-  const int64_t q = qt * 32 + (l & 31);
-  const bool qvalid = q < nq;
-  const float sg = knn_scale(scal);
-  const float inv_s2 = 1.f / (sg * sg);  // exact: sigma is a power of two
-
-  // B operand (queries): B[k = 16 s + 8h + j][col = l&31] = sigma q_f (f<d), 1 (f==d), 0.
-  f16x8 bhi[KS16], blo[KS16];
-#pragma unroll
-  for (int s = 0; s < KS16; ++s)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int f = 16 * s + 8 * h + j;
-      const float v = qvalid ? ((f < d) ? sg * query[q * d + f] : ((f == d) ? 1.f : 0.f)) : 0.f;
-      _Float16 a, b;
-      split_f16(v, a, b);
-      bhi[s][j] = a;
-      blo[s][j] = b;
-    }
-  // Retire the B-operand loads here and launder the registers, so no compiler-tracked load is
-  // pending inside the tile loop (otherwise its waitcnt pass drains vmcnt(0) every iteration).
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int s = 0; s < KS16; ++s) {
-    f32x4 x = __builtin_bit_cast(f32x4, bhi[s]);
-    f32x4 y = __builtin_bit_cast(f32x4, blo[s]);
-    asm volatile("" : "+v"(x), "+v"(y));
-    bhi[s] = __builtin_bit_cast(f16x8, x);
-    blo[s] = __builtin_bit_cast(f16x8, y);
-  }
-
-  float ld[LIST];
-  int li[LIST];
-#pragma unroll
-  for (int j = 0; j < LIST; ++j) {
-    ld[j] = INFINITY;
-    li[j] = -1;
-  }
-  const float thr0 = INFINITY;
-  float thr = thr0;
-  int cnt = 0;
-
-  const int64_t t0 = (int64_t)sp * tiles_per_split;
-  const int64_t t1 = min(nct, t0 + tiles_per_split);
-
-  // Fragment buffers in registers: tile t's MFMAs run while tile t-1's threshold work executes
-  // and the next tiles' loads are in flight; a buffer is refilled only after the chain that
-  // read it has completed.  Loads are inline asm with hand-counted waits (NV per tile; no other
-  // vector-memory op in the loop).  Three buffers, two where a 4-k-step tile and long lists
-  // would otherwise reach the 256-VGPR cap (at the cap the asm-load buffers are not safe from
-  // register copies).
-  constexpr int NV = NH * KS16;  // dwordx4 per lane per tile: one per (k-step, half)
-  constexpr int NB = NH == 2 ? (KS16 >= 4 ? 2 : 3) : ((KS16 >= 4 && LIST > 32) ? 2 : 3);
-  const f32x4* abase = reinterpret_cast<const f32x4*>(apack) + l;
-  f32x4 Bf[NB][NV];
-  auto load = [&](f32x4 (&A)[NV], int64_t t) {
-    const f32x4* p = abase + t * 64 * NV;
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      f32x4 x;
-      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(x) : "v"(p + v * 64) : "memory");
-      A[v] = x;
-    }
-  };
-  auto landed = [&](f32x4 (&A)[NV]) {  // all but the NV youngest loads (next tile) have landed
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NV) : "memory");
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      f32x4 x = A[v];
-      asm volatile("" : "+v"(x));
-      A[v] = x;
-    }
-  };
-  auto chain = [&](const f32x4 (&A)[NV]) -> f32x16 {
-    f32x16 acc = {};
-#pragma unroll
-    for (int s = 0; s < KS16; ++s) {
-      const f16x8 ah = __builtin_bit_cast(f16x8, A[NH * s]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bhi[s], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, blo[s], acc, 0, 0, 0);
-      if constexpr (NH == 2) {
-        const f16x8 al = __builtin_bit_cast(f16x8, A[2 * s + 1]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bhi[s], acc, 0, 0, 0);
-      }
-    }
-    return acc;
-  };
-  auto process = [&](f32x16 acc, int64_t t) {
-    float m = fminf(fminf(fminf(acc[0], acc[1]), fminf(acc[2], acc[3])),
-                    fminf(fminf(acc[4], acc[5]), fminf(acc[6], acc[7])));
-    m = fminf(m, fminf(fminf(fminf(acc[8], acc[9]), fminf(acc[10], acc[11])),
-                       fminf(fminf(acc[12], acc[13]), fminf(acc[14], acc[15]))));
-    if (__ballot(m < thr)) {
-      const int base = (int)(t * 32);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        if (acc[r] < thr) {
-          sbuf_v[w][cnt][l] = acc[r];
-          sbuf_i[w][cnt][l] = base + acc_row(r, l);
-          ++cnt;
-        }
-      }
-      if (__ballot(cnt > kBufCap - 16))
-        flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0, keep);
-    }
-  };
-  if constexpr (NB == 2) {
-    if (t0 < t1) {
-      // Double buffer: tile t+1's loads are issued right after tile t's MFMA chain (the chain
-      // of t-1, the last reader of that buffer, executed before chain t in the matrix pipe)
-      // and land while the chain and the threshold work of t-1 run; each step then waits for
-      // all outstanding loads, which are exactly tile t's.
-      const int64_t tl = t1 - 1;
-      load(Bf[0], t0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[0][v]));
-      f32x16 accP = chain(Bf[0]);
-      load(Bf[1], min(t0 + 1, tl));
-      int64_t t = t0 + 1;
-#define MEPOL_SEL16_STEP2(CUR, NXT)                            \
-  {                                                           \
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          \
-    _Pragma("unroll") for (int v = 0; v < NV; ++v)            \
-        asm volatile("" : "+v"(Bf[CUR][v]));                  \
-    const f32x16 accN = chain(Bf[CUR]);                       \
-    load(Bf[NXT], min(t + 1, tl));                            \
-    process(accP, t - 1);                                     \
-    accP = accN;                                              \
-    ++t;                                                      \
-  }
-#pragma nounroll
-      while (t + 1 < t1) {
-        MEPOL_SEL16_STEP2(1, 0)
-        MEPOL_SEL16_STEP2(0, 1)
-      }
-      if (t < t1) MEPOL_SEL16_STEP2(1, 0)
-#undef MEPOL_SEL16_STEP2
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[b][v]));
-      process(accP, t - 1);
-    }
-  } else if (t0 < t1) {
-    const int64_t tl = t1 - 1;
-    load(Bf[0], t0);
-    load(Bf[1], min(t0 + 1, tl));
-    landed(Bf[0]);
-    f32x16 accP = chain(Bf[0]);
-    load(Bf[2], min(t0 + 2, tl));
-    int64_t t = t0 + 1;
-    // steady state, unrolled by 3 so buffer indices are compile-time: at step t the tile is in
-    // Bf[(t - t0) % 3], the chain of t-1 read Bf[(t - t0 - 1) % 3] (refilled with t+2).
-#define MEPOL_SEL16_STEP(CUR, PREV)         \
-  {                                         \
-    landed(Bf[CUR]);                        \
-    const f32x16 accN = chain(Bf[CUR]);     \
-    process(accP, t - 1);                   \
-    load(Bf[PREV], min(t + 2, tl));         \
-    accP = accN;                            \
-    ++t;                                    \
-  }
-#pragma nounroll
-    while (t + 2 < t1) {
-      MEPOL_SEL16_STEP(1, 0)
-      MEPOL_SEL16_STEP(2, 1)
-      MEPOL_SEL16_STEP(0, 2)
-    }
-    // remainder (0..2 tiles), same buffer rotation
-    if (t < t1) MEPOL_SEL16_STEP(1, 0)
-    if (t < t1) MEPOL_SEL16_STEP(2, 1)
-#undef MEPOL_SEL16_STEP
-    // Retire every outstanding fragment load and keep all three buffers live up to here: the
-    // last prefetches are never consumed, and an asm load whose output the compiler thinks is
-    // dead may be given registers that a later instruction reuses while the data is in flight.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[b][v]));
-    process(accP, t - 1);
-  }
-  flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0, keep);
-
-  if (qvalid) {
-    // The last slot carries this lane's final bound: every candidate of its range that is not
-    // in the list has an approximate value >= min(list last, thr) (rejected against thr, or
-    // evicted from the list); a last entry at or above the bound is dropped (idx -1), the
-    // bound covers it.  refine takes the min over the query's lanes.
-    const float bound = fminf(ld[LIST - 1], thr);
-    const int64_t o = ((q * split + sp) * 2 + h) * LIST;
-#pragma unroll
-    for (int j = 0; j < LIST - 1; ++j) {
-      out_v[o + j] = ld[j] * inv_s2;
-      out_i[o + j] = li[j];
-    }
-    out_v[o + LIST - 1] = bound * inv_s2;
-    out_i[o + LIST - 1] = (bound < ld[LIST - 1]) ? -1 : li[LIST - 1];
   }
 }
 
@@ -1058,40 +729,6 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   return 0;
 }
 
-static int select_occ3() {
-  const char* e = getenv("MEPOL_KNN_OCC3");
-  return !(e && e[0] == '0');
-}
-
-template <int KS16, int NH>
-static void launch_select16_ks(const Plan& P, const _Float16* ap, const float* query,
-                               const unsigned* scal, float* lv, int* li, hipStream_t st) {
-  const dim3 g((unsigned)((P.nqt + 3) / 4), (unsigned)P.split);
-#define MEPOL_SEL16O(L, O)                                                                       \
-  hipLaunchKernelGGL((select16_kernel<KS16, L, NH, O>), g, dim3(256), 0, st, ap, query, P.nq,     \
-                     P.d, P.nct, P.split, P.tiles_per_split, P.keep, scal, lv, li)
-#define MEPOL_SEL16(L) MEPOL_SEL16O(L, 1)
-  switch (P.LIST16) {  // >= keep + 4 >= 7; split-candidate plans keep the instances that fit
-    case 8: MEPOL_SEL16(8); break;
-    case 16: MEPOL_SEL16(16); break;
-    case 24:
-      if constexpr (NH == 1 && KS16 <= 2) {
-        if (select_occ3()) {
-          MEPOL_SEL16O(24, 3);
-          break;
-        }
-      }
-      MEPOL_SEL16(24);
-      break;
-    case 32: MEPOL_SEL16(32); break;
-    default:
-      if constexpr (NH == 1 || KS16 <= 2) MEPOL_SEL16(40);
-      break;
-  }
-#undef MEPOL_SEL16
-#undef MEPOL_SEL16O
-}
-
 // MEPOL_KNN_RANK_MERGE=0 selects the argmin-round merge in refine_kernel (A/B probe).
 static int refine_rank_merge() {
   static const int v = [] {
@@ -1236,19 +873,14 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
   hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, cand,
                      P.nc, P.d, P.KS16, P.nh, P.nct, ap16, cmax, cpad, P.dp);
   MEPOL_CHECK_LAUNCH();
-  if (P.nh == 1) {
+  {
+    const SelectArgs sa{ap16,        query,  P.nq,   P.d,    P.nct, P.split, P.tiles_per_split,
+                        P.keep,      P.LIST16, P.nh, P.nqt,  cmax,  lv,      li};
     switch (P.KS16) {
-      case 1: launch_select16_ks<1, 1>(P, ap16, query, cmax, lv, li, st); break;
-      case 2: launch_select16_ks<2, 1>(P, ap16, query, cmax, lv, li, st); break;
-      case 3: launch_select16_ks<3, 1>(P, ap16, query, cmax, lv, li, st); break;
-      default: launch_select16_ks<4, 1>(P, ap16, query, cmax, lv, li, st); break;
-    }
-  } else {
-    switch (P.KS16) {
-      case 1: launch_select16_ks<1, 2>(P, ap16, query, cmax, lv, li, st); break;
-      case 2: launch_select16_ks<2, 2>(P, ap16, query, cmax, lv, li, st); break;
-      case 3: launch_select16_ks<3, 2>(P, ap16, query, cmax, lv, li, st); break;
-      default: launch_select16_ks<4, 2>(P, ap16, query, cmax, lv, li, st); break;
+      case 1: launch_select<1>(sa, st); break;
+      case 2: launch_select<2>(sa, st); break;
+      case 3: launch_select<3>(sa, st); break;
+      default: launch_select<4>(sa, st); break;
     }
   }
   MEPOL_CHECK_LAUNCH();

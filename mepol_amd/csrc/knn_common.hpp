@@ -1,0 +1,128 @@
+// Shared pieces of the k-NN translation units (knn.hip: pack / refine / exact / dispatch;
+// knn_select_ks{1..4}.hip: the selection kernels, one TU per k-step count so they build in
+// parallel).  See knn.hip for the pipeline.
+#pragma once
+#include "common.hpp"
+
+#include <algorithm>
+#include <cfloat>
+#include <climits>
+#include <cmath>
+#include <cstdlib>
+
+namespace mepol {
+namespace knn {
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+using f32x4 = __attribute__((ext_vector_type(4))) float;
+using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
+
+constexpr int kBufCap = 24;        // per-lane LDS insertion buffer (entries)
+constexpr int kMaxSplit = 16;
+constexpr int kExactGrid = 512;    // blocks of the exhaustive fallback (exact_kernel)
+constexpr int kRefineList = 64;    // approximate candidates refine ranks per query (one wave)
+
+// ---------------------------------------------------------------------------------------
+// 2. select: list helpers
+// ---------------------------------------------------------------------------------------
+template <int LIST>
+__device__ __forceinline__ void list_insert(float (&ld)[LIST], int (&li)[LIST], float x, int xi) {
+  // ld ascending; precondition x < ld[LIST-1].  Branch-free shift-insert.
+  bool c[LIST];
+#pragma unroll
+  for (int j = 0; j < LIST; ++j) c[j] = x < ld[j];
+#pragma unroll
+  for (int j = LIST - 1; j >= 1; --j) {
+    ld[j] = c[j - 1] ? ld[j - 1] : (c[j] ? x : ld[j]);
+    li[j] = c[j - 1] ? li[j - 1] : (c[j] ? xi : li[j]);
+  }
+  ld[0] = c[0] ? x : ld[0];
+  li[0] = c[0] ? xi : li[0];
+}
+
+// Merge this lane's LDS buffer into its sorted list; then share the prune bound with the
+// partner lane (l ^ 32 serves the same query column).  Every lane of the wave calls it.
+// keep > 0 (split-f16 select): the bound also takes max(own keep-th, partner's keep-th): the
+// two half lists then hold >= 2 keep values at or below it, so 2 keep >= kp1 + slack of the
+// query's candidates in this range are never pruned; this bound is far tighter than a list's
+// own last entry (the LIST-th of one half).  The bound only decreases over the scan.
+template <int LIST>
+__device__ __forceinline__ float list_at(const float (&ld)[LIST], int j) {
+  float v = INFINITY;
+#pragma unroll
+  for (int i = 0; i < LIST; ++i) v = (i == j) ? ld[i] : v;
+  return v;
+}
+
+template <int LIST>
+__device__ __forceinline__ void flush_buffer(float (&ld)[LIST], int (&li)[LIST], float& thr, int& cnt,
+                                             const float (*bv)[64], const int (*bi)[64], int l,
+                                             float thr0, int keep = 0) {
+  const int mc = wave_max_i(cnt);
+#pragma nounroll
+  for (int e = 0; e < mc; ++e) {
+    if (e < cnt) {
+      const float x = bv[e][l];
+      const int xi = bi[e][l];
+      if (x < thr) {
+        list_insert<LIST>(ld, li, x, xi);
+        thr = ld[LIST - 1];
+      }
+    }
+  }
+  cnt = 0;
+  // lanes l and l^32 serve the same query: the tighter of their maxima is a valid prune bound
+  // for both (refine's certification bound is the min over all lanes' final bounds and the
+  // query's sampled bound thr0).
+  thr = fminf(thr0, fminf(ld[LIST - 1], __shfl_xor(ld[LIST - 1], 32, kWave)));
+  if (keep > 0) {
+    const float kv = list_at<LIST>(ld, keep - 1);
+    thr = fminf(thr, fmaxf(kv, __shfl_xor(kv, 32, kWave)));
+  }
+}
+
+// Row (candidate within the tile) of accumulator register r for lane l (32x32 C/D map).
+__device__ __forceinline__ int acc_row(int r, int l) { return (r & 3) + 8 * (r >> 2) + 4 * (l >> 5); }
+
+// sigma = 2^e with sigma * max(cmax, qmax) in (64, 128] (1 when the data is all zero).
+__device__ __forceinline__ float knn_scale(const unsigned* __restrict__ scal) {
+  const float m = fmaxf(__uint_as_float(scal[0]), __uint_as_float(scal[2]));
+  // slack for the f32 rounding of sqrt in norms_kernel: 127.9 instead of 128
+  if (!(m > 0.f) || !(m < 3e38f)) return 1.f;
+  int e;
+  (void)frexpf(127.9f / m, &e);
+  e = max(-100, min(100, e - 1));
+  return ldexpf(1.f, e);
+}
+
+__device__ __forceinline__ void split_f16(float v, _Float16& hi, _Float16& lo) {
+  hi = (_Float16)v;
+  lo = (_Float16)(v - (float)hi);  // v - hi is exact in f32
+}
+
+constexpr float kPadNorm16 = 60000.f;  // scaled |c|^2 of padding candidates (> any real D')
+
+// Arguments of the selection launch (make_plan's fields the select kernels read).
+struct SelectArgs {
+  const _Float16* apack;
+  const float* query;
+  int64_t nq;
+  int d;
+  int64_t nct;
+  int split;
+  int64_t tiles_per_split;
+  int keep;
+  int LIST16;
+  int nh;
+  int64_t nqt;
+  const unsigned* scal;
+  float* out_v;
+  int* out_i;
+};
+
+// knn_select_ks<KS16>.hip
+template <int KS16>
+void launch_select(const SelectArgs& a, hipStream_t st);
+
+}  // namespace knn
+}  // namespace mepol

@@ -1,0 +1,9 @@
+// Selection kernels for k-step count 4 (d + 1 <= 64): one TU per count so the
+// instances build in parallel.
+#include "knn_select.hpp"
+
+namespace mepol {
+namespace knn {
+template void launch_select<4>(const SelectArgs& a, hipStream_t st);
+}  // namespace knn
+}  // namespace mepol
