@@ -405,15 +405,20 @@ def run(args):
     knn_desc = (("f16 MFMA selection (candidate hi half x split query" if plan["nh"] == 1 else
                  "f16 MFMA selection (split candidate x split query, 3 products")
                 + ", f32 accumulate) + certified f64 exact refine (bit-exact output)")
-    traffic = None
+    traffic, traffic_note = None, None
     pmc_path = os.path.join(ROOT, "profiles", f"knn_pmc_{args.workload}.json")
-    if args.workload == "C3" and not os.path.exists(pmc_path):
-        pmc_path = os.path.join(ROOT, "profiles", "knn_pmc.json")
     if os.path.exists(pmc_path) and world == 1:  # counters were taken on the 1-GPU k-NN call
+        # the PMC passes (tools/knn_pmc.sh -> tools/knn_pmc_summary.py) stamp the file with a
+        # hash of the k-NN sources they measured; a file from other sources is not reported
         try:
-            traffic = json.load(open(pmc_path)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+            pmc = json.load(open(pmc_path))
+            if pmc.get("knn_source_stamp") == knn_source_stamp():
+                traffic = pmc.get("hbm_bytes_per_launch")
+            else:
+                traffic_note = (f"{os.path.relpath(pmc_path, ROOT)} was measured on other k-NN "
+                                "sources (stamp mismatch): not reported")
+        except Exception as e:
+            traffic_note = f"unreadable {pmc_path}: {e!r}"
     rehearsal = sharded and backend != "nccl" and world > 1
     line = {
         "metric": f"MEPOL epoch wall-clock ({args.workload}: N={N}, d={d}, k={k}"
@@ -446,7 +451,10 @@ def run(args):
                      "kernel": "k-NN call (norms + pack + select + refine + exact), HIP events on "
                                "the launch stream; achieved = F/t, F = 3*d*Nq*Nc (SURVEY 8d)"},
     }
+    if traffic_note:
+        line["roofline"]["traffic_note"] = traffic_note
     if traffic:
+        line["roofline"]["traffic_source"] = os.path.relpath(pmc_path, ROOT)
         gbps = traffic / (knn_ms * 1e-3) / 1e9
         line["roofline"]["hbm_GBps"] = round(gbps, 1)
         line["roofline"]["hbm_frac"] = round(gbps / PEAK_HBM_GBPS, 4)
@@ -465,6 +473,20 @@ def run(args):
     _emit(line)
     if dist is not None:
         parallel.destroy_process_group(dist)
+
+
+def knn_source_stamp():
+    """Hash of the k-NN sources (csrc/knn*.hip / *.hpp): ties a PMC traffic file to the code it
+    was measured on (the GPU box has the sources but no git history)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "mepol_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.startswith("knn") or f == "common.hpp":
+            h.update(f.encode())
+            h.update(open(os.path.join(csrc, f), "rb").read())
+    return h.hexdigest()[:16]
 
 
 PEAK_F64_TFLOPS = 78.6            # MI355X spec: FP64 matrix (dense)
@@ -614,6 +636,12 @@ def cpu_baseline(cfg, sample_queries, iters_done):
     return {"value": round(epoch_s, 3), "unit": "s/epoch", "cores": cores, "kind": "port",
             "sample": sample + "; torch f64 CPU", "cpu_model": _cpu_model(),
             "affinity_cpus": aff,
+            # SURVEY 8(d) asks for all affinity CPUs; the box's declared CPU share is
+            # OMP_NUM_THREADS (16 per GPU), which the harness asks worker pools to respect.  The
+            # measured value uses the share; this is the same epoch at perfect scaling to every
+            # affinity CPU (a lower bound on the CPU time there), so the GPU/CPU ratio lies
+            # between the two.
+            "value_ideal_at_affinity": round(epoch_s * cores / aff, 3),
             "components_s": {"rollout": round(roll_s, 3), "knn": round(knn_s, 3),
                              "policy_update": round(upd_s, 3), "compute_kl": round(kl_s, 3),
                              "iterations": iters},

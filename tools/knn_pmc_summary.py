@@ -11,6 +11,7 @@ import sqlite3
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 
 
 def per_call(db, counter):
@@ -36,11 +37,17 @@ def main(src="gpurun_out"):
     kernels = {k: {"fetch_bytes_raw": fetch.get(k), "fetch_bytes_x2": 2 * fetch.get(k, 0.0),
                    "write_bytes": write.get(k)} for k in sorted(set(fetch) | set(write))}
     total = sum(2 * v for v in fetch.values()) + sum(write.values())
+    from bench import knn_source_stamp
+
     out = {"hbm_bytes_per_launch": total, "kernels": kernels,
+           "knn_source_stamp": knn_source_stamp(),
            "workload": "C3 k-NN: N=200000 queries x 200000 candidates, d=29, k+1=31",
            "correction": "FETCH_SIZE x2 (gfx950), WRITE_SIZE x1; KiB -> bytes"}
-    path = os.path.join(ROOT, "profiles", "knn_pmc_C3.json")
-    json.dump(out, open(path, "w"), indent=1)
+    # profiles/ for a bench.py later in the same GPU call; a copy next to the counters, which
+    # gpurun brings back (commit it as profiles/knn_pmc_C3.json)
+    for path in (os.path.join(ROOT, "profiles", "knn_pmc_C3.json"),
+                 os.path.join(src, "knn_pmc_C3.json")):
+        json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
 
