@@ -192,6 +192,32 @@ int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double*
                               double* db1, void* workspace, size_t workspace_bytes,
                               void* stream);
 
+/* The same with dz2 formed on chip instead of read: dz2[n][j] = [z2 + b2 > 0] sum_a
+ * coef[n][a] Wm[a][j] from the forward's z2 [n, k] (pre-bias), b2 [k] (16-byte aligned),
+ * Wm [a_dim, k] and coef [n, a_dim] = dL/dmu (mepol_head_coef); a_dim <= 8. */
+int mepol_dh1_layer1_backward_formed(const double* z2, const double* b2, const double* Wm,
+                                     const double* coef, int a_dim, int64_t n, int k,
+                                     const double* W2t, int hidden0, const double* h1,
+                                     const double* x, int in_features, double* dW1, double* db1,
+                                     void* workspace, size_t workspace_bytes, void* stream);
+
+/* Policy-head backward without writing dz2 (round 4; replaces mepol_head_backward + the dW2
+ * GEMM of loss.backward(), mepol.py:278, policy.py:43-51, for action_dim <= 8).  One workspace
+ * (mepol_head_grad_workspace_size) carries the coefficients c = dL/dmu [n, a_dim] between the
+ * two stages: mepol_head_coef (grad_logp [n], act / mu [n, a_dim], log_std [a_dim]) on the
+ * caller's stream, then mepol_head_dw2 (may run on a forked stream next to
+ * mepol_dh1_layer1_backward_formed): dW2 [h1w, h0] = dz2^T h1, db2 [h1w] (nullable),
+ * dWm [a_dim, h1w], dbm [a_dim], dlog_std [a_dim], with dz2 formed on chip from z2 [n, h1w]
+ * (pre-bias), b2, Wm and c.  Fixed-order reductions. */
+int mepol_head_grad_workspace_size(int64_t n, int h1w, int h0, int a_dim, size_t* bytes);
+int mepol_head_coef(const double* grad_logp, const double* act, const double* mu,
+                    const double* log_std, int64_t n, int a_dim, void* workspace,
+                    size_t workspace_bytes, void* stream);
+int mepol_head_dw2(const double* z2, const double* b2, const double* Wm, const double* h1,
+                   int64_t n, int h1w, int h0, int a_dim, double* dW2, double* db2, double* dWm,
+                   double* dbm, double* dlog_std, void* workspace, size_t workspace_bytes,
+                   void* stream);
+
 /* Hidden layer on the f64 matrix cores: C = act(A B^T + bias), A [n, k] (row stride lda),
  * B [m, k] (ldb), bias [m] (nullable), C [n, m] (ldc); act = ReLU when relu != 0.  k, lda, ldb
  * even and A, B 16-byte aligned.  variant 0 = default tiling.  Replaces the torch.mm /

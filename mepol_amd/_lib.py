@@ -56,6 +56,13 @@ SIGNATURES = {
     "mepol_dh1_layer1_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
     "mepol_dh1_layer1_backward": [_c_vp, _c_i64, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
                                   _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
+    "mepol_dh1_layer1_backward_formed": [_c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_int,
+                                         _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
+                                         _c_vp, _c_sz, _c_vp],
+    "mepol_head_grad_workspace_size": [_c_i64, _c_int, _c_int, _c_int, ctypes.POINTER(_c_sz)],
+    "mepol_head_coef": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_sz, _c_vp],
+    "mepol_head_dw2": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_int, _c_vp, _c_vp,
+                       _c_vp, _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_gemm_nt": [_c_vp, _c_i64, _c_int, _c_i64, _c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_vp,
                       _c_i64, _c_int, _c_vp],
     "mepol_step_mountaincar": [_c_vp, _c_vp, _c_i64, _c_i64, _c_vp],

@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
 // ---------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------
-static int select_occ3() {
+static inline int select_occ3() {
   const char* e = getenv("MEPOL_KNN_OCC3");
   return !(e && e[0] == '0');
 }

@@ -269,7 +269,7 @@ class ShardedEpoch:
             return None
         if self.dist.get_backend(self.group) != "nccl":  # only RCCL collectives can be captured
             return None
-        if os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") != "0":
+        if self.dist is torch.distributed and os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") != "0":
             # the group recycles events across capture and eager use (prepare_nccl_env): a
             # captured graph would put the watchdog thread at risk, so stay eager
             if not _GRAPH_STATE.get("warned"):
