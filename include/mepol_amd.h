@@ -99,6 +99,12 @@ int mepol_entropy_forward(const double* w, const int32_t* idxT, const double* D,
                           int64_t n_w, int k, int kp1, double ns, double G, double B, double eps,
                           double* W_out, double* g_out, double* partials, double* out4,
                           void* stream);
+/* The same with out4 updated in place and vals[2] = {out4[0] on entry (the previous pass's H),
+ * the new KL}: the off-policy graph iteration's two control scalars (device_loop.py). */
+int mepol_entropy_forward_emit(const double* w, const int32_t* idxT, const double* D, int64_t n,
+                               int64_t n_w, int k, int kp1, double ns, double G, double B,
+                               double eps, double* W_out, double* g_out, double* partials,
+                               double* out4, double* vals, void* stream);
 
 /* ---- entropy gradient (the autograd of policy_update's loss.backward(), mepol.py:278) ----
  * CSR transpose of the first k rows of idxT ([>=k, nq]) for owned ids [col_offset, +ncand):
@@ -194,10 +200,11 @@ int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double*
 
 /* The same with dz2 formed on chip instead of read: dz2[n][j] = [z2 + b2 > 0] sum_a
  * coef[n][a] Wm[a][j] from the forward's z2 [n, k] (pre-bias), b2 [k] (16-byte aligned),
- * Wm [a_dim, k] and coef [n, a_dim] = dL/dmu (mepol_head_coef); a_dim <= 8. */
+ * Wm [a_dim, k] and coef [n, a_dim] = dL/dmu (mepol_head_coef); a_dim <= 8.  Takes W2 [k, hidden0]
+ * itself (hidden0 even), not its transpose. */
 int mepol_dh1_layer1_backward_formed(const double* z2, const double* b2, const double* Wm,
                                      const double* coef, int a_dim, int64_t n, int k,
-                                     const double* W2t, int hidden0, const double* h1,
+                                     const double* W2, int hidden0, const double* h1,
                                      const double* x, int in_features, double* dW1, double* db1,
                                      void* workspace, size_t workspace_bytes, void* stream);
 

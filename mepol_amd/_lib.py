@@ -35,6 +35,8 @@ SIGNATURES = {
     "mepol_entropy_partials_size": [_c_i64],
     "mepol_entropy_forward": [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_dbl, _c_dbl,
                               _c_dbl, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
+    "mepol_entropy_forward_emit": [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_dbl, _c_dbl,
+                              _c_dbl, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
     "mepol_csr_workspace_size": [_c_i64, _c_int, _c_i64, ctypes.POINTER(_c_sz)],
     "mepol_csr_build": [_c_vp, _c_i64, _c_int, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_sz,
                         _c_vp],

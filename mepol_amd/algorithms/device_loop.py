@@ -125,7 +125,7 @@ class DeviceIteration:
         # by the dW2 kernel and the dh1 kernel from z2, c = dL/dmu, Wm and b2
         b2 = self.named[3]
         self.fused_head = (self.fused_dh1 and ops.head_grad_ok(Wm.shape[0])
-                           and b2.data_ptr() % 16 == 0
+                           and b2.data_ptr() % 16 == 0 and W1.shape[0] % 2 == 0
                            and os.environ.get("MEPOL_FUSED_HEAD", "1") != "0")
         self.ws_hg = (ops.head_grad_workspace(self.N, W2.shape[0], W1.shape[0], Wm.shape[0], dev)
                       if self.fused_head else None)
@@ -296,9 +296,6 @@ class DeviceIteration:
         layer-1 backward, and than splitting dW2 across both phases)."""
         W1, b1, W2, b2, Wm, bm, ls = self.named
         cur = torch.cuda.current_stream()
-        # W2^T for the fused dh1 kernel, on this stream: on a forked one the small copy kernel
-        # would queue behind the dW2 GEMM's workgroups
-        W2t = W2.t().contiguous() if self.fused_dh1 else None
         if self.fused_head:
             # c = dL/dmu (and the dbm / dlog_std partials), then dW2 / db2 / dWm on the forked
             # stream next to the dh1 + layer-1 backward, both forming dz2 on chip
@@ -308,11 +305,14 @@ class DeviceIteration:
             with torch.cuda.stream(self.fork):
                 dW2, db2, dWm, dbm, dls = ops.head_dw2(self.z2, b2, Wm, self.h1, self.ws_hg)
             with torch.cuda.stream(self.s_gemm):
-                dW1, db1 = ops.dh1_layer1_backward_formed(self.z2, b2, Wm, self.ws_hg, W2t,
+                dW1, db1 = ops.dh1_layer1_backward_formed(self.z2, b2, Wm, self.ws_hg, W2,
                                                           self.h1, self.x, ws_dh1=self.ws_dh1)
             cur.wait_stream(self.fork)
             cur.wait_stream(self.s_gemm)
             return dW1, db1, dW2, db2, dWm, dbm, dls
+        # W2^T for the fused dh1 kernel, on this stream: on a forked one the small copy kernel
+        # would queue behind the dW2 GEMM's workgroups
+        W2t = W2.t().contiguous() if self.fused_dh1 else None
         self.fork.wait_stream(cur)
         self.s_gemm.wait_stream(cur)
         dz2, dWm, dbm, dls, db2 = ops.head_backward(grad, self.z2, Wm, ls, self.act, self.mu,
@@ -358,10 +358,11 @@ class DeviceIteration:
         # (w_cur and g_cur were last read by this replay's gamma / reverse scan, above)
         self.forward()
         ops.iw_forward(lt, self.logp_b, self.offsets, N, w_out=self.w_cur)
-        out2, _, _ = ops.entropy_forward(self.w_cur, self.idx32T, self.D, k, self.ns, self.G,
-                                         self.B, self.eps, g_out=self.g_cur)
-        # (H(theta_t), KL(theta_t+1)) to the host, theta_t+1's sums kept for the next replay
-        self._emit(self.out_cur, 0, out2, 1, self.out_cur, out2, 4)
+        # (H(theta_t), KL(theta_t+1)) into vals by the entropy pass itself, theta_t+1's sums
+        # kept in out_cur for the next replay, then vals to the host
+        ops.entropy_forward(self.w_cur, self.idx32T, self.D, k, self.ns, self.G, self.B,
+                            self.eps, g_out=self.g_cur, out4=self.out_cur, vals=self.vals)
+        ops.memcpy_async(self.vals_host, self.vals)
 
     def _optim_step(self, grads):
         """optimizer.step() (mepol.py:280).  The kernel also leaves theta_t in the replay's

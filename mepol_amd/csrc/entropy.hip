@@ -146,10 +146,13 @@ __global__ __launch_bounds__(256) void entropy_fwd_kernel(
 
 // out[0] = H = -sum(term) + B ; out[1] = KL (unclamped) = sum(kl_term)/N_w ;
 // out[2] = sum(term) ; out[3] = sum(kl_term)  (raw sums for multi-rank reduction)
+// vals (nullable, the graph iteration's control scalars): vals[0] = the H that out[0] held on
+// entry (H(theta_t) of the previous pass), vals[1] = the new KL; out is then overwritten.
 __global__ __launch_bounds__(256) void entropy_finalize_kernel(const double* __restrict__ partials,
                                                                int64_t nblocks, double B,
                                                                int64_t N_w,
-                                                               double* __restrict__ out) {
+                                                               double* __restrict__ out,
+                                                               double* __restrict__ vals) {
   __shared__ double sh[4];
   double a = 0.0, b = 0.0;
   for (int64_t i = threadIdx.x; i < nblocks; i += blockDim.x) {
@@ -168,6 +171,10 @@ __global__ __launch_bounds__(256) void entropy_finalize_kernel(const double* __r
   if (threadIdx.x == 0) {
     const double ta = sh[0] + sh[1] + sh[2] + sh[3];
     const double tb = sb[0] + sb[1] + sb[2] + sb[3];
+    if (vals) {
+      vals[0] = out[0];
+      vals[1] = (1.0 / (double)N_w) * tb;
+    }
     out[0] = -ta + B;
     out[1] = (1.0 / (double)N_w) * tb;
     out[2] = ta;
@@ -300,10 +307,10 @@ extern "C" int mepol_entropy_partials_size(int64_t n_particles) {
 
 // w: [N_w] (all particles, global indexing); idxT: [kp1][n] transposed neighbour indices of the
 // n local query particles; D: [n][kp1].  out4 = {H, KL_unclamped, sum term, sum kl_term}.
-extern "C" int mepol_entropy_forward(const double* w, const int32_t* idxT, const double* D,
-                                     int64_t n, int64_t n_w, int k, int kp1, double ns, double G,
-                                     double B, double eps, double* W_out, double* g_out,
-                                     double* partials, double* out4, void* stream) {
+static int entropy_forward_impl(const double* w, const int32_t* idxT, const double* D, int64_t n,
+                                int64_t n_w, int k, int kp1, double ns, double G, double B,
+                                double eps, double* W_out, double* g_out, double* partials,
+                                double* out4, double* vals, void* stream) {
   if (n < 0 || k <= 0 || kp1 <= k || !w || !idxT || !D || !W_out || !g_out || !partials || !out4) {
     set_error("mepol_entropy_forward: bad arguments");
     return kErrBadArg;
@@ -316,9 +323,33 @@ extern "C" int mepol_entropy_forward(const double* w, const int32_t* idxT, const
                        n_w, k, kp1, ns, pi_ns2_over_G, eps, W_out, g_out, partials);
     MEPOL_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(entropy_finalize_kernel, dim3(1), dim3(256), 0, st, partials, nb, B, n_w, out4);
+  hipLaunchKernelGGL(entropy_finalize_kernel, dim3(1), dim3(256), 0, st, partials, nb, B, n_w, out4,
+                     vals);
   MEPOL_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int mepol_entropy_forward(const double* w, const int32_t* idxT, const double* D,
+                                     int64_t n, int64_t n_w, int k, int kp1, double ns, double G,
+                                     double B, double eps, double* W_out, double* g_out,
+                                     double* partials, double* out4, void* stream) {
+  return entropy_forward_impl(w, idxT, D, n, n_w, k, kp1, ns, G, B, eps, W_out, g_out, partials,
+                              out4, nullptr, stream);
+}
+
+// The graph iteration's form: out4 is updated in place and vals = {H held on entry, new KL}
+// (the two control scalars the host reads), with no separate stack / copy launches.
+extern "C" int mepol_entropy_forward_emit(const double* w, const int32_t* idxT, const double* D,
+                                          int64_t n, int64_t n_w, int k, int kp1, double ns,
+                                          double G, double B, double eps, double* W_out,
+                                          double* g_out, double* partials, double* out4,
+                                          double* vals, void* stream) {
+  if (!vals) {
+    set_error("mepol_entropy_forward_emit: vals is null");
+    return kErrBadArg;
+  }
+  return entropy_forward_impl(w, idxT, D, n, n_w, k, kp1, ns, G, B, eps, W_out, g_out, partials,
+                              out4, vals, stream);
 }
 
 // gamma over the n_own particles this rank owns (CSR over its own ids), partial S per block.

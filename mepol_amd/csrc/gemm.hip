@@ -53,7 +53,10 @@ struct FormArgs {
 };
 constexpr int kFormA = 8;
 
-template <int WR, int WC, int FR, int FC, int FORM = 0>
+// BT = 1: B is given transposed, Bt [K][M] row-major (ldb = its row stride): the dh1 GEMM takes
+// W2 [h1w][h0] as it is, with no W2^T copy per iteration.  Chunks are (k, column pair) there and
+// are transposed on their way into LDS.
+template <int WR, int WC, int FR, int FC, int FORM = 0, int BT = 0>
 __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int64_t N, int K,
                                               int64_t lda, const double* __restrict__ B, int M,
                                               int64_t ldb, int64_t row0, int col0, double* lds,
@@ -93,9 +96,16 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
     }
 #pragma unroll
     for (int p = 0; p < P::PB; ++p) {
-      const int ch = min(tid + p * T, P::CB - 1), r = ch >> 3, k = kb + 2 * (ch & 7);
-      rb[p] = *reinterpret_cast<const double2*>(B + (int64_t)min(col0 + r, M - 1) * ldb +
-                                                min(k, k2));
+      const int ch = min(tid + p * T, P::CB - 1);
+      if constexpr (BT) {
+        const int kk = ch / (BN / 2), mp = 2 * (ch % (BN / 2));
+        rb[p] = *reinterpret_cast<const double2*>(B + (int64_t)min(kb + kk, K - 1) * ldb +
+                                                  min(col0 + mp, M - 2));
+      } else {
+        const int r = ch >> 3, k = kb + 2 * (ch & 7);
+        rb[p] = *reinterpret_cast<const double2*>(B + (int64_t)min(col0 + r, M - 1) * ldb +
+                                                  min(k, k2));
+      }
     }
   };
   auto lstore = [&](int kt, int buf) __attribute__((always_inline)) {
@@ -139,11 +149,20 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
     }
 #pragma unroll
     for (int p = 0; p < P::PB; ++p) {
-      const int ch = tid + p * T, r = ch >> 3, k = kb + 2 * (ch & 7);
+      const int ch = tid + p * T;
       if (ch < P::CB) {
-        const bool ok = col0 + r < M && k < K;
-        *reinterpret_cast<double2*>(sB + (buf * BN + r) * KP + 2 * (ch & 7)) =
-            ok ? rb[p] : double2{0.0, 0.0};
+        if constexpr (BT) {
+          const int kk = ch / (BN / 2), mp = 2 * (ch % (BN / 2));
+          const bool kok = kb + kk < K;
+          // LDS row = column m, position = k within the tile (same layout as the NT path)
+          sB[(buf * BN + mp) * KP + kk] = (kok && col0 + mp < M) ? rb[p].x : 0.0;
+          sB[(buf * BN + mp + 1) * KP + kk] = (kok && col0 + mp + 1 < M) ? rb[p].y : 0.0;
+        } else {
+          const int r = ch >> 3, k = kb + 2 * (ch & 7);
+          const bool ok = col0 + r < M && k < K;
+          *reinterpret_cast<double2*>(sB + (buf * BN + r) * KP + 2 * (ch & 7)) =
+              ok ? rb[p] : double2{0.0, 0.0};
+        }
       }
     }
   };
@@ -256,7 +275,9 @@ __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
   const int64_t row0 = (int64_t)rb * BM;
   const int col0 = (tile % ncb) * BN;
   d4 acc[FR][FC];
-  gemm_mainloop<WR, WC, FR, FC, FORM>(dz2, N, K, K, W2t, M, K, row0, col0, lds, acc, fa);
+  // FORM: the formed variant also takes W2 [K][M] itself (BT) instead of W2^T
+  gemm_mainloop<WR, WC, FR, FC, FORM, FORM>(dz2, N, K, K, W2t, M, FORM ? M : K, row0, col0, lds,
+                                            acc, fa);
 
   // B operands [x | 1] for k-step (i, q): lane (fr, g) holds x[row(i, q, g)][16 h + fr]
   double xb[FR][4][NH];
@@ -485,14 +506,19 @@ extern "C" int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, co
 }
 
 // The same with dz2 formed on chip (head_grad.hip): z2 [n][k] pre-bias from the forward, b2 [k],
-// Wm [a_dim][k], coef [n][a_dim] = dL/dmu from mepol_head_coef (a_dim <= 8).
+// Wm [a_dim][k], coef [n][a_dim] = dL/dmu from mepol_head_coef (a_dim <= 8), and W2 [k][m]
+// itself (not its transpose; m even).
 extern "C" int mepol_dh1_layer1_backward_formed(const double* z2, const double* b2,
                                                 const double* Wm, const double* coef, int a_dim,
-                                                int64_t n, int k, const double* W2t, int m,
+                                                int64_t n, int k, const double* W2, int m,
                                                 const double* h1, const double* x,
                                                 int in_features, double* dW1, double* db1,
                                                 void* workspace, size_t workspace_bytes,
                                                 void* stream) {
-  return dh1_layer1_backward_impl<1>(z2, n, k, W2t, m, h1, x, in_features, dW1, db1, workspace,
+  if (m & 1) {
+    mepol::set_error("mepol_dh1_layer1_backward_formed: hidden0 must be even");
+    return mepol::kErrBadArg;
+  }
+  return dh1_layer1_backward_impl<1>(z2, n, k, W2, m, h1, x, in_features, dW1, db1, workspace,
                                      workspace_bytes, stream, FormArgs{coef, Wm, b2, a_dim});
 }

@@ -159,10 +159,11 @@ def iw_normalize(u, U, out=None):
     return w
 
 
-def entropy_forward(w, idxT, D, k, ns, G, B, eps, n_w=None, g_out=None):
+def entropy_forward(w, idxT, D, k, ns, G, B, eps, n_w=None, g_out=None, out4=None, vals=None):
     """Fused compute_entropy + compute_kl forward.
 
-    Returns (out4 f64[4] = {H, KL_unclamped, sum_term, sum_klterm}, W [n], g [n]).
+    Returns (out4 f64[4] = {H, KL_unclamped, sum_term, sum_klterm}, W [n], g [n]).  With `vals`
+    (f64[2]) and `out4` given, out4 is updated in place and vals = {out4[0] on entry, new KL}.
     """
     _require_device(w, idxT, D)
     n = D.shape[0]
@@ -174,7 +175,13 @@ def entropy_forward(w, idxT, D, k, ns, G, B, eps, n_w=None, g_out=None):
     partials = torch.empty(max(2 * nparts, 2), dtype=torch.float64, device=dev)
     W = torch.empty(n, dtype=torch.float64, device=dev)
     g = g_out if g_out is not None else torch.empty(n, dtype=torch.float64, device=dev)
-    out4 = torch.empty(4, dtype=torch.float64, device=dev)
+    if vals is not None:
+        assert out4 is not None
+        call("mepol_entropy_forward_emit", ptr(w.contiguous()), ptr(idxT), ptr(D.contiguous()), n,
+             n_w, k, kp1, float(ns), float(G), float(B), float(eps), ptr(W), ptr(g),
+             ptr(partials), ptr(out4), ptr(vals), _stream())
+        return out4, W, g
+    out4 = out4 if out4 is not None else torch.empty(4, dtype=torch.float64, device=dev)
     call("mepol_entropy_forward", ptr(w.contiguous()), ptr(idxT), ptr(D.contiguous()), n, n_w, k,
          kp1, float(ns), float(G), float(B), float(eps), ptr(W), ptr(g), ptr(partials), ptr(out4),
          _stream())
@@ -351,13 +358,14 @@ def head_dw2(z2, b2, Wm, h1, ws, dW2=None, db2=None, dWm=None, dbm=None, dls=Non
     return dW2, db2, dWm, dbm, dls
 
 
-def dh1_layer1_backward_formed(z2, b2, Wm, ws, W2t, h1, x, ws_dh1=None):
-    """dh1_layer1_backward with dz2 formed on chip (coefficients from head_coef in `ws`)."""
+def dh1_layer1_backward_formed(z2, b2, Wm, ws, W2, h1, x, ws_dh1=None):
+    """dh1_layer1_backward with dz2 formed on chip (coefficients from head_coef in `ws`); takes
+    W2 [h1w, h0] itself (no transpose)."""
     n, k = z2.shape
-    h0 = W2t.shape[0]
+    h0 = W2.shape[1]
     f = x.shape[1]
     a = Wm.shape[0]
-    assert W2t.shape[1] == k and h1.shape == (n, h0) and z2.is_contiguous()
+    assert W2.shape[0] == k and h1.shape == (n, h0) and z2.is_contiguous() and W2.is_contiguous()
     if ws_dh1 is None:
         import ctypes
 
@@ -367,7 +375,7 @@ def dh1_layer1_backward_formed(z2, b2, Wm, ws, W2t, h1, x, ws_dh1=None):
     dW = torch.empty((h0, f), dtype=torch.float64, device=x.device)
     db = torch.empty(h0, dtype=torch.float64, device=x.device)
     call("mepol_dh1_layer1_backward_formed", ptr(z2), ptr(b2), ptr(Wm.contiguous()), ptr(ws), a,
-         n, k, ptr(W2t), h0, ptr(h1), ptr(x), f, ptr(dW), ptr(db), ptr(ws_dh1), ws_dh1.numel(),
+         n, k, ptr(W2), h0, ptr(h1), ptr(x), f, ptr(dW), ptr(db), ptr(ws_dh1), ws_dh1.numel(),
          _stream())
     return dW, db
 

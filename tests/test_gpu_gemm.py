@@ -87,7 +87,7 @@ def test_fused_head_backward_matches_round3_path_and_torch(cuda, n, nf, h0, h1w,
     ws = ops.head_grad_workspace(n, h1w, h0, a, x.device)
     ops.head_coef(grad, act, mu, ls, ws)
     dW2, db2, dWm, dbm, dls = ops.head_dw2(z2, b2, Wm, h1, ws)
-    dW1, db1 = ops.dh1_layer1_backward_formed(z2, b2, Wm, ws, W2t, h1, x)
+    dW1, db1 = ops.dh1_layer1_backward_formed(z2, b2, Wm, ws, W2, h1, x)
     # the formed dz2 is head_bwd's dz2 bit for bit, so dh1 / dW1 only differ by nothing
     assert torch.equal(dW1, dW1_r) and torch.equal(db1, db1_r)
     for got, ref in ((dW2, dW2_r), (db2, db2_r), (dWm, dWm_r), (dbm, dbm_r), (dls, dls_r)):
