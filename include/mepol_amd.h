@@ -105,6 +105,14 @@ int mepol_entropy_forward_emit(const double* w, const int32_t* idxT, const doubl
                                int64_t n_w, int k, int kp1, double ns, double G, double B,
                                double eps, double* W_out, double* g_out, double* partials,
                                double* out4, double* vals, void* stream);
+/* Sharded off-policy iteration (mepol_amd/parallel.py), one launch each: the all-gathered
+ * per-rank [u (n) | sum u] blocks normalised into w_glob [world n] (U summed in rank order), and
+ * the replay's control scalars from the all-gathered raw sums (at offset off of each rank's block
+ * of `stride` doubles): vals = {B - sums_cur[0], sum_kl / n_global}, then sums_cur = the sums. */
+int mepol_iw_normalize_gathered(const double* xu_all, int world, int64_t n, double* w_glob,
+                                void* stream);
+int mepol_sharded_emit(const double* x_all, int world, int64_t stride, int64_t off, double B,
+                       int64_t n_global, double* sums_cur, double* vals, void* stream);
 
 /* ---- entropy gradient (the autograd of policy_update's loss.backward(), mepol.py:278) ----
  * CSR transpose of the first k rows of idxT ([>=k, nq]) for owned ids [col_offset, +ncand):
@@ -197,33 +205,6 @@ int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double*
                               const double* h1, const double* x, int in_features, double* dW1,
                               double* db1, void* workspace, size_t workspace_bytes,
                               void* stream);
-
-/* The same with dz2 formed on chip instead of read: dz2[n][j] = [z2 + b2 > 0] sum_a
- * coef[n][a] Wm[a][j] from the forward's z2 [n, k] (pre-bias), b2 [k] (16-byte aligned),
- * Wm [a_dim, k] and coef [n, a_dim] = dL/dmu (mepol_head_coef); a_dim <= 8.  Takes W2 [k, hidden0]
- * itself (hidden0 even), not its transpose. */
-int mepol_dh1_layer1_backward_formed(const double* z2, const double* b2, const double* Wm,
-                                     const double* coef, int a_dim, int64_t n, int k,
-                                     const double* W2, int hidden0, const double* h1,
-                                     const double* x, int in_features, double* dW1, double* db1,
-                                     void* workspace, size_t workspace_bytes, void* stream);
-
-/* Policy-head backward without writing dz2 (round 4; replaces mepol_head_backward + the dW2
- * GEMM of loss.backward(), mepol.py:278, policy.py:43-51, for action_dim <= 8).  One workspace
- * (mepol_head_grad_workspace_size) carries the coefficients c = dL/dmu [n, a_dim] between the
- * two stages: mepol_head_coef (grad_logp [n], act / mu [n, a_dim], log_std [a_dim]) on the
- * caller's stream, then mepol_head_dw2 (may run on a forked stream next to
- * mepol_dh1_layer1_backward_formed): dW2 [h1w, h0] = dz2^T h1, db2 [h1w] (nullable),
- * dWm [a_dim, h1w], dbm [a_dim], dlog_std [a_dim], with dz2 formed on chip from z2 [n, h1w]
- * (pre-bias), b2, Wm and c.  Fixed-order reductions. */
-int mepol_head_grad_workspace_size(int64_t n, int h1w, int h0, int a_dim, size_t* bytes);
-int mepol_head_coef(const double* grad_logp, const double* act, const double* mu,
-                    const double* log_std, int64_t n, int a_dim, void* workspace,
-                    size_t workspace_bytes, void* stream);
-int mepol_head_dw2(const double* z2, const double* b2, const double* Wm, const double* h1,
-                   int64_t n, int h1w, int h0, int a_dim, double* dW2, double* db2, double* dWm,
-                   double* dbm, double* dlog_std, void* workspace, size_t workspace_bytes,
-                   void* stream);
 
 /* Hidden layer on the f64 matrix cores: C = act(A B^T + bias), A [n, k] (row stride lda),
  * B [m, k] (ldb), bias [m] (nullable), C [n, m] (ldc); act = ReLU when relu != 0.  k, lda, ldb

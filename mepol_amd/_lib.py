@@ -37,6 +37,8 @@ SIGNATURES = {
                               _c_dbl, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
     "mepol_entropy_forward_emit": [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_dbl, _c_dbl,
                               _c_dbl, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
+    "mepol_iw_normalize_gathered": [_c_vp, _c_int, _c_i64, _c_vp, _c_vp],
+    "mepol_sharded_emit": [_c_vp, _c_int, _c_i64, _c_i64, _c_dbl, _c_i64, _c_vp, _c_vp, _c_vp],
     "mepol_csr_workspace_size": [_c_i64, _c_int, _c_i64, ctypes.POINTER(_c_sz)],
     "mepol_csr_build": [_c_vp, _c_i64, _c_int, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_sz,
                         _c_vp],
@@ -58,13 +60,6 @@ SIGNATURES = {
     "mepol_dh1_layer1_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
     "mepol_dh1_layer1_backward": [_c_vp, _c_i64, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
                                   _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
-    "mepol_dh1_layer1_backward_formed": [_c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_i64, _c_int,
-                                         _c_vp, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
-                                         _c_vp, _c_sz, _c_vp],
-    "mepol_head_grad_workspace_size": [_c_i64, _c_int, _c_int, _c_int, ctypes.POINTER(_c_sz)],
-    "mepol_head_coef": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_sz, _c_vp],
-    "mepol_head_dw2": [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_int, _c_vp, _c_vp,
-                       _c_vp, _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_gemm_nt": [_c_vp, _c_i64, _c_int, _c_i64, _c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_vp,
                       _c_i64, _c_int, _c_vp],
     "mepol_step_mountaincar": [_c_vp, _c_vp, _c_i64, _c_i64, _c_vp],

@@ -121,14 +121,6 @@ class DeviceIteration:
                           and os.environ.get("MEPOL_FUSED_FWD", "1") != "0")
         self.fused_dh1 = (ops.dh1_layer1_ok(self.x.shape[1], W2.shape[0])
                           and os.environ.get("MEPOL_FUSED_DH1", "1") != "0")
-        # head backward without the dz2 round trip (csrc/head_grad.hip): dz2 is formed on chip
-        # by the dW2 kernel and the dh1 kernel from z2, c = dL/dmu, Wm and b2
-        b2 = self.named[3]
-        self.fused_head = (self.fused_dh1 and ops.head_grad_ok(Wm.shape[0])
-                           and b2.data_ptr() % 16 == 0 and W1.shape[0] % 2 == 0
-                           and os.environ.get("MEPOL_FUSED_HEAD", "1") != "0")
-        self.ws_hg = (ops.head_grad_workspace(self.N, W2.shape[0], W1.shape[0], Wm.shape[0], dev)
-                      if self.fused_head else None)
         self.neg_one = torch.full((), -1.0, **f64)
         # every body takes its optimizer step through _optim_step, which leaves theta_t in the
         # replay's shadow (off_policy_optimization then copies it into last_valid only when it
@@ -296,20 +288,6 @@ class DeviceIteration:
         layer-1 backward, and than splitting dW2 across both phases)."""
         W1, b1, W2, b2, Wm, bm, ls = self.named
         cur = torch.cuda.current_stream()
-        if self.fused_head:
-            # c = dL/dmu (and the dbm / dlog_std partials), then dW2 / db2 / dWm on the forked
-            # stream next to the dh1 + layer-1 backward, both forming dz2 on chip
-            ops.head_coef(grad, self.act, self.mu, ls, self.ws_hg)
-            self.fork.wait_stream(cur)
-            self.s_gemm.wait_stream(cur)
-            with torch.cuda.stream(self.fork):
-                dW2, db2, dWm, dbm, dls = ops.head_dw2(self.z2, b2, Wm, self.h1, self.ws_hg)
-            with torch.cuda.stream(self.s_gemm):
-                dW1, db1 = ops.dh1_layer1_backward_formed(self.z2, b2, Wm, self.ws_hg, W2,
-                                                          self.h1, self.x, ws_dh1=self.ws_dh1)
-            cur.wait_stream(self.fork)
-            cur.wait_stream(self.s_gemm)
-            return dW1, db1, dW2, db2, dWm, dbm, dls
         # W2^T for the fused dh1 kernel, on this stream: on a forked one the small copy kernel
         # would queue behind the dW2 GEMM's workgroups
         W2t = W2.t().contiguous() if self.fused_dh1 else None

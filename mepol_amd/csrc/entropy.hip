@@ -378,3 +378,60 @@ extern "C" int mepol_entropy_reverse_scan(const double* gamma, const double* w,
   MEPOL_CHECK_LAUNCH();
   return 0;
 }
+
+// ---- sharded iteration helpers (parallel.py ShardedIteration, one launch each) -------------
+// w_glob[r n + i] = xu_all[r (n + 1) + i] / U, U = sum_r xu_all[r (n + 1) + n] in rank order:
+// the all-gathered [u | sum u] blocks of every rank normalised in one pass (no copy, no sum).
+__global__ void iw_normalize_gathered_kernel(const double* __restrict__ xu_all, int world,
+                                             int64_t n, double* __restrict__ w_glob) {
+  double U = 0.0;
+  for (int r = 0; r < world; ++r) U += xu_all[(int64_t)r * (n + 1) + n];
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)world * n) return;
+  const int64_t r = e / n, i = e % n;
+  w_glob[e] = xu_all[r * (n + 1) + i] / U;
+}
+
+// The two control scalars of a sharded replay from the all-gathered raw sums (stride apart,
+// at offset off of each rank's block): sums = rank-order sums, vals = {B - sums_cur[0] (the H
+// of the previous pass), sums[1] / N_global (the new KL)}, then sums_cur = sums.
+__global__ void sharded_emit_kernel(const double* __restrict__ x_all, int world, int64_t stride,
+                                    int64_t off, double B, int64_t n_global,
+                                    double* __restrict__ sums_cur, double* __restrict__ vals) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s0 = 0.0, s1 = 0.0;
+  for (int r = 0; r < world; ++r) {
+    s0 += x_all[(int64_t)r * stride + off];
+    s1 += x_all[(int64_t)r * stride + off + 1];
+  }
+  vals[0] = B - sums_cur[0];
+  vals[1] = s1 / (double)n_global;
+  sums_cur[0] = s0;
+  sums_cur[1] = s1;
+}
+
+extern "C" int mepol_iw_normalize_gathered(const double* xu_all, int world, int64_t n,
+                                           double* w_glob, void* stream) {
+  if (world <= 0 || n <= 0 || !xu_all || !w_glob) {
+    set_error("mepol_iw_normalize_gathered: bad arguments");
+    return kErrBadArg;
+  }
+  const int64_t tot = (int64_t)world * n;
+  hipLaunchKernelGGL(iw_normalize_gathered_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256),
+                     0, (hipStream_t)stream, xu_all, world, n, w_glob);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int mepol_sharded_emit(const double* x_all, int world, int64_t stride, int64_t off,
+                                  double B, int64_t n_global, double* sums_cur, double* vals,
+                                  void* stream) {
+  if (world <= 0 || off + 1 >= stride || !x_all || !sums_cur || !vals) {
+    set_error("mepol_sharded_emit: bad arguments");
+    return kErrBadArg;
+  }
+  hipLaunchKernelGGL(sharded_emit_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, x_all, world,
+                     stride, off, B, n_global, sums_cur, vals);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}

@@ -40,27 +40,11 @@ struct Cfg {
 // fragment j]^T over all of K for the workgroup tile (row0, col0).  Operand loads read clamped
 // (always valid) addresses; out-of-range values are zeroed when the registers are written to
 // LDS, after the MFMA block, so no select waits on a load right after issuing it.
-// FORM = 1 (the dh1 kernel of the fused head backward, head_grad.hip): A is not read from
-// memory but formed per element from the forward's z2 (pre-bias) and the head coefficients:
-//   A[n][k] = [z2[n][k] + b2[k] > 0] sum_a coef[n][a] Wm[a][k]      (= dz2, never written)
-// with head_bwd_kernel's arithmetic.  The block's coefficient rows (sC [BM][8]) and Wm^T
-// (sWt [K][8]) sit in LDS behind the operand tiles.
-struct FormArgs {
-  const double* coef;  // [N][A]
-  const double* Wm;    // [A][K]
-  const double* b2;    // [K]
-  int A;               // <= 8
-};
-constexpr int kFormA = 8;
-
-// BT = 1: B is given transposed, Bt [K][M] row-major (ldb = its row stride): the dh1 GEMM takes
-// W2 [h1w][h0] as it is, with no W2^T copy per iteration.  Chunks are (k, column pair) there and
-// are transposed on their way into LDS.
-template <int WR, int WC, int FR, int FC, int FORM = 0, int BT = 0>
+template <int WR, int WC, int FR, int FC>
 __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int64_t N, int K,
                                               int64_t lda, const double* __restrict__ B, int M,
                                               int64_t ldb, int64_t row0, int col0, double* lds,
-                                              d4 (&acc)[FR][FC], FormArgs fa = FormArgs{}) {
+                                              d4 (&acc)[FR][FC]) {
   using P = Cfg<WR, WC, FR, FC>;
   constexpr int T = P::kThreads, BM = P::BM, BN = P::BN;
   double* sA = lds;                  // [2][BM][KP]
@@ -69,21 +53,6 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
   const int wr = wave / WC, wc = wave % WC;
   const int nkt = (K + KT - 1) / KT;
   const int k2 = K - 2;  // last 16-B aligned pair start (K even)
-
-  double* sC = lds + 2 * (BM + BN) * KP;  // FORM: [BM][kFormA] coefficient rows
-  double* sWt = sC + BM * kFormA;           // FORM: [K][kFormA] Wm^T
-  if constexpr (FORM) {
-    for (int e = tid; e < BM * kFormA; e += T) {
-      const int r = e / kFormA, a = e % kFormA;
-      const int64_t n = min<int64_t>(row0 + r, N - 1);
-      sC[e] = a < fa.A ? fa.coef[n * fa.A + a] : 0.0;
-    }
-    for (int e = tid; e < K * kFormA; e += T) {
-      const int k = e / kFormA, a = e % kFormA;
-      sWt[e] = a < fa.A ? fa.Wm[(int64_t)a * K + k] : 0.0;
-    }
-    __syncthreads();
-  }
 
   double2 ra[P::PA], rb[P::PB];
   auto gload = [&](int kt) __attribute__((always_inline)) {
@@ -96,48 +65,13 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
     }
 #pragma unroll
     for (int p = 0; p < P::PB; ++p) {
-      const int ch = min(tid + p * T, P::CB - 1);
-      if constexpr (BT) {
-        const int kk = ch / (BN / 2), mp = 2 * (ch % (BN / 2));
-        rb[p] = *reinterpret_cast<const double2*>(B + (int64_t)min(kb + kk, K - 1) * ldb +
-                                                  min(col0 + mp, M - 2));
-      } else {
-        const int r = ch >> 3, k = kb + 2 * (ch & 7);
-        rb[p] = *reinterpret_cast<const double2*>(B + (int64_t)min(col0 + r, M - 1) * ldb +
-                                                  min(k, k2));
-      }
+      const int ch = min(tid + p * T, P::CB - 1), r = ch >> 3, k = kb + 2 * (ch & 7);
+      rb[p] = *reinterpret_cast<const double2*>(B + (int64_t)min(col0 + r, M - 1) * ldb +
+                                                min(k, k2));
     }
   };
   auto lstore = [&](int kt, int buf) __attribute__((always_inline)) {
     const int kb = kt * KT;
-    if constexpr (FORM) {
-      // every chunk of this thread has the same column pair (ch & 7 = tid & 7)
-      const int k = min(kb + 2 * (tid & 7), K - 2);
-      double w0[kFormA], w1[kFormA];
-#pragma unroll
-      for (int a = 0; a < kFormA; ++a) {
-        w0[a] = sWt[k * kFormA + a];
-        w1[a] = sWt[(k + 1) * kFormA + a];
-      }
-      const double2 bb = *reinterpret_cast<const double2*>(fa.b2 + k);
-#pragma unroll
-      for (int p = 0; p < P::PA; ++p) {
-        const int ch = tid + p * T, r = ch >> 3;
-        if (ch < P::CA) {
-          double d0 = 0.0, d1 = 0.0;
-#pragma unroll
-          for (int a = 0; a < kFormA; ++a) {
-            if (a < fa.A) {
-              const double c = sC[r * kFormA + a];
-              d0 = fma(c, w0[a], d0);
-              d1 = fma(c, w1[a], d1);
-            }
-          }
-          ra[p].x = (ra[p].x + bb.x > 0.0) ? d0 : 0.0;
-          ra[p].y = (ra[p].y + bb.y > 0.0) ? d1 : 0.0;
-        }
-      }
-    }
 #pragma unroll
     for (int p = 0; p < P::PA; ++p) {
       const int ch = tid + p * T, r = ch >> 3, k = kb + 2 * (ch & 7);
@@ -149,20 +83,11 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
     }
 #pragma unroll
     for (int p = 0; p < P::PB; ++p) {
-      const int ch = tid + p * T;
+      const int ch = tid + p * T, r = ch >> 3, k = kb + 2 * (ch & 7);
       if (ch < P::CB) {
-        if constexpr (BT) {
-          const int kk = ch / (BN / 2), mp = 2 * (ch % (BN / 2));
-          const bool kok = kb + kk < K;
-          // LDS row = column m, position = k within the tile (same layout as the NT path)
-          sB[(buf * BN + mp) * KP + kk] = (kok && col0 + mp < M) ? rb[p].x : 0.0;
-          sB[(buf * BN + mp + 1) * KP + kk] = (kok && col0 + mp + 1 < M) ? rb[p].y : 0.0;
-        } else {
-          const int r = ch >> 3, k = kb + 2 * (ch & 7);
-          const bool ok = col0 + r < M && k < K;
-          *reinterpret_cast<double2*>(sB + (buf * BN + r) * KP + 2 * (ch & 7)) =
-              ok ? rb[p] : double2{0.0, 0.0};
-        }
+        const bool ok = col0 + r < M && k < K;
+        *reinterpret_cast<double2*>(sB + (buf * BN + r) * KP + 2 * (ch & 7)) =
+            ok ? rb[p] : double2{0.0, 0.0};
       }
     }
   };
@@ -259,11 +184,11 @@ constexpr int WR = 8, WC = 1, FR = 2, FC = 5;
 using P = Cfg<WR, WC, FR, FC>;
 }  // namespace l1b
 
-template <int NH, int FORM = 0>  // NH = ceil((F + 1) / 16) column groups of [x | 1]
+template <int NH>  // NH = ceil((F + 1) / 16) column groups of [x | 1]
 __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
     const double* __restrict__ dz2, int64_t N, int K, const double* __restrict__ W2t, int M,
     const double* __restrict__ h1, const double* __restrict__ x, int F,
-    double* __restrict__ part, FormArgs fa = FormArgs{}) {
+    double* __restrict__ part) {
   using namespace l1b;
   constexpr int BM = P::BM, BN = P::BN, T = P::kThreads;
   extern __shared__ double lds[];
@@ -275,9 +200,7 @@ __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
   const int64_t row0 = (int64_t)rb * BM;
   const int col0 = (tile % ncb) * BN;
   d4 acc[FR][FC];
-  // FORM: the formed variant also takes W2 [K][M] itself (BT) instead of W2^T
-  gemm_mainloop<WR, WC, FR, FC, FORM, FORM>(dz2, N, K, K, W2t, M, FORM ? M : K, row0, col0, lds,
-                                            acc, fa);
+  gemm_mainloop<WR, WC, FR, FC>(dz2, N, K, K, W2t, M, K, row0, col0, lds, acc);
 
   // B operands [x | 1] for k-step (i, q): lane (fr, g) holds x[row(i, q, g)][16 h + fr]
   double xb[FR][4][NH];
@@ -438,23 +361,19 @@ extern "C" int mepol_dh1_layer1_workspace_size(int64_t n, int m, int in_features
   return 0;
 }
 
-template <int FORM>
-static int dh1_layer1_backward_impl(const double* dz2, int64_t n, int k, const double* W2t,
-                                    int m, const double* h1, const double* x, int in_features,
-                                    double* dW1, double* db1, void* workspace,
-                                    size_t workspace_bytes, void* stream, FormArgs fa) {
+extern "C" int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double* W2t,
+                                         int m, const double* h1, const double* x,
+                                         int in_features, double* dW1, double* db1,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
   using namespace mepol::gemm::l1b;
   using mepol::gemm::dh1_layer1_bwd_kernel;
   const int F = in_features;
   if (n <= 0 || k <= 0 || (k & 1) || m <= 0 || F <= 0 || F > 63 || !dz2 || !W2t || !h1 || !x ||
-      !dW1 || !workspace || ((uintptr_t)dz2 & 15) || ((uintptr_t)W2t & 15) ||
-      (FORM && (!fa.coef || !fa.Wm || !fa.b2 || fa.A <= 0 || fa.A > kFormA ||
-                ((uintptr_t)fa.b2 & 15)))) {
+      !dW1 || !workspace || ((uintptr_t)dz2 & 15) || ((uintptr_t)W2t & 15)) {
     mepol::set_error("mepol_dh1_layer1_backward: bad arguments (k even, in_features <= 63, "
-                     "16-B aligned dz2 / W2t / b2, action_dim <= %d)", kFormA);
+                     "16-B aligned dz2 / W2t)");
     return mepol::kErrBadArg;
   }
-  const size_t lds = P::kLds + (FORM ? ((size_t)P::BM + k) * kFormA * sizeof(double) : 0);
   const int nrb = (int)((n + P::BM - 1) / P::BM);
   const size_t need = ((size_t)nrb + mepol::gemm::kGroups) * m * (F + 1) * sizeof(double);
   if (workspace_bytes < need) {
@@ -470,12 +389,12 @@ static int dh1_layer1_backward_impl(const double* dz2, int64_t n, int k, const d
   do {                                                                                         \
     static bool attr = false;                                                                  \
     if (!attr) {                                                                               \
-      MEPOL_HIP(hipFuncSetAttribute((const void*)dh1_layer1_bwd_kernel<NHV, FORM>,             \
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));  \
+      MEPOL_HIP(hipFuncSetAttribute((const void*)dh1_layer1_bwd_kernel<NHV>,                   \
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)P::kLds)); \
       attr = true;                                                                             \
     }                                                                                          \
-    hipLaunchKernelGGL((dh1_layer1_bwd_kernel<NHV, FORM>), dim3(tiles), dim3(P::kThreads), lds, \
-                       st, dz2, n, k, W2t, m, h1, x, F, part, fa);                             \
+    hipLaunchKernelGGL(dh1_layer1_bwd_kernel<NHV>, dim3(tiles), dim3(P::kThreads), P::kLds, st, \
+                       dz2, n, k, W2t, m, h1, x, F, part);                                     \
   } while (0)
   switch (nh) {
     case 1: MEPOL_L1B(1); break;
@@ -495,30 +414,4 @@ static int dh1_layer1_backward_impl(const double* dz2, int64_t n, int k, const d
                      dim3(256), 0, st, grp, m, F, dW1, db1);
   MEPOL_CHECK_LAUNCH();
   return 0;
-}
-
-extern "C" int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double* W2t,
-                                         int m, const double* h1, const double* x,
-                                         int in_features, double* dW1, double* db1,
-                                         void* workspace, size_t workspace_bytes, void* stream) {
-  return dh1_layer1_backward_impl<0>(dz2, n, k, W2t, m, h1, x, in_features, dW1, db1, workspace,
-                                     workspace_bytes, stream, FormArgs{});
-}
-
-// The same with dz2 formed on chip (head_grad.hip): z2 [n][k] pre-bias from the forward, b2 [k],
-// Wm [a_dim][k], coef [n][a_dim] = dL/dmu from mepol_head_coef (a_dim <= 8), and W2 [k][m]
-// itself (not its transpose; m even).
-extern "C" int mepol_dh1_layer1_backward_formed(const double* z2, const double* b2,
-                                                const double* Wm, const double* coef, int a_dim,
-                                                int64_t n, int k, const double* W2, int m,
-                                                const double* h1, const double* x,
-                                                int in_features, double* dW1, double* db1,
-                                                void* workspace, size_t workspace_bytes,
-                                                void* stream) {
-  if (m & 1) {
-    mepol::set_error("mepol_dh1_layer1_backward_formed: hidden0 must be even");
-    return mepol::kErrBadArg;
-  }
-  return dh1_layer1_backward_impl<1>(z2, n, k, W2, m, h1, x, in_features, dW1, db1, workspace,
-                                     workspace_bytes, stream, FormArgs{coef, Wm, b2, a_dim});
 }

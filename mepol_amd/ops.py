@@ -188,6 +188,20 @@ def entropy_forward(w, idxT, D, k, ns, G, B, eps, n_w=None, g_out=None, out4=Non
     return out4, W, g
 
 
+def iw_normalize_gathered(xu_all, world, n, w_out):
+    """w_out [world n] <- the all-gathered [u | sum u] blocks (world x (n + 1)) normalised by
+    the rank-order sum of their totals."""
+    call("mepol_iw_normalize_gathered", ptr(xu_all), world, n, ptr(w_out), _stream())
+    return w_out
+
+
+def sharded_emit(x_all, world, stride, off, B, n_global, sums_cur, vals):
+    """vals <- (B - sums_cur[0], rank-order sum of x_all[r, off + 1] / n_global);
+    sums_cur <- the rank-order sums of x_all[r, off], x_all[r, off + 1]."""
+    call("mepol_sharded_emit", ptr(x_all), world, stride, off, float(B), n_global, ptr(sums_cur),
+         ptr(vals), _stream())
+
+
 def csr_build(idxT, k, n_own, col_offset=0, row_offset=0, nq=None):
     """CSR transpose of the first k rows of idxT ([>=k, nq]) for ids [col_offset, +n_own)."""
     import ctypes
@@ -314,69 +328,6 @@ def dh1_layer1_backward(dz2, W2t, h1, x, ws=None):
     db = torch.empty(h0, dtype=torch.float64, device=x.device)
     call("mepol_dh1_layer1_backward", ptr(dz2), n, k, ptr(W2t), h0, ptr(h1), ptr(x), f, ptr(dW),
          ptr(db), ptr(ws), ws.numel(), _stream())
-    return dW, db
-
-
-HEAD_GRAD_MAX_A = 8
-
-
-def head_grad_ok(a_dim):
-    return a_dim <= HEAD_GRAD_MAX_A
-
-
-def head_grad_workspace(n, h1w, h0, a_dim, device):
-    """Caller-owned workspace of the fused head backward (coefficients + dW2 records)."""
-    import ctypes
-
-    nbytes = ctypes.c_size_t()
-    call("mepol_head_grad_workspace_size", n, h1w, h0, a_dim, ctypes.byref(nbytes))
-    return torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=device)
-
-
-def head_coef(grad_logp, act, mu, log_std, ws):
-    """Stage 1 of the fused head backward: c = dL/dmu [n, a] into `ws` (and the dbm / dlog_std
-    partials), on the current stream."""
-    n, a = act.shape
-    call("mepol_head_coef", ptr(grad_logp.contiguous()), ptr(act), ptr(mu), ptr(log_std), n, a,
-         ptr(ws), ws.numel(), _stream())
-
-
-def head_dw2(z2, b2, Wm, h1, ws, dW2=None, db2=None, dWm=None, dbm=None, dls=None):
-    """Stage 2: (dW2 [h1w, h0], db2, dWm [a, h1w], dbm, dlog_std) with dz2 = dL/dz2 formed on
-    chip from z2 (pre-bias), b2, Wm and the coefficients head_coef left in `ws`."""
-    n, h1w = z2.shape
-    h0 = h1.shape[1]
-    a = Wm.shape[0]
-    f64 = dict(dtype=torch.float64, device=z2.device)
-    dW2 = dW2 if dW2 is not None else torch.empty((h1w, h0), **f64)
-    db2 = db2 if db2 is not None else torch.empty(h1w, **f64)
-    dWm = dWm if dWm is not None else torch.empty((a, h1w), **f64)
-    dbm = dbm if dbm is not None else torch.empty(a, **f64)
-    dls = dls if dls is not None else torch.empty(a, **f64)
-    call("mepol_head_dw2", ptr(z2), ptr(b2), ptr(Wm.contiguous()), ptr(h1), n, h1w, h0, a,
-         ptr(dW2), ptr(db2), ptr(dWm), ptr(dbm), ptr(dls), ptr(ws), ws.numel(), _stream())
-    return dW2, db2, dWm, dbm, dls
-
-
-def dh1_layer1_backward_formed(z2, b2, Wm, ws, W2, h1, x, ws_dh1=None):
-    """dh1_layer1_backward with dz2 formed on chip (coefficients from head_coef in `ws`); takes
-    W2 [h1w, h0] itself (no transpose)."""
-    n, k = z2.shape
-    h0 = W2.shape[1]
-    f = x.shape[1]
-    a = Wm.shape[0]
-    assert W2.shape[0] == k and h1.shape == (n, h0) and z2.is_contiguous() and W2.is_contiguous()
-    if ws_dh1 is None:
-        import ctypes
-
-        nbytes = ctypes.c_size_t()
-        call("mepol_dh1_layer1_workspace_size", n, h0, f, ctypes.byref(nbytes))
-        ws_dh1 = _workspace(x.device, nbytes.value, tag="dh1l1")
-    dW = torch.empty((h0, f), dtype=torch.float64, device=x.device)
-    db = torch.empty(h0, dtype=torch.float64, device=x.device)
-    call("mepol_dh1_layer1_backward_formed", ptr(z2), ptr(b2), ptr(Wm.contiguous()), ptr(ws), a,
-         n, k, ptr(W2), h0, ptr(h1), ptr(x), f, ptr(dW), ptr(db), ptr(ws_dh1), ws_dh1.numel(),
-         _stream())
     return dW, db
 
 

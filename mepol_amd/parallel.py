@@ -335,10 +335,15 @@ class ShardedIteration(DeviceIteration):
       1. all-gather of one f64: the per-rank partial of S = sum_j gamma_j w_j   (8 B per rank)
       2. all-reduce of the flattened policy gradients                       (~1.1 MB at C3)
       3. all-gather of [u (n_local), sum u]: unnormalised weights + normaliser (n_local + 1 f64)
-      4. all-gather of [dH/dW (n_local), H-sum, KL-sum]                        (n_local + 2 f64)
+      4. all-gather of [dH/dW (n_local), H, KL, H-sum, KL-sum]                 (n_local + 4 f64)
 
     Reductions over ranks are fixed-order sums of gathered values, so every rank holds the same
-    bits and takes the same accept/backtrack branch (mepol.py:441-476)."""
+    bits and takes the same accept/backtrack branch (mepol.py:441-476).  The gathered blocks are
+    read where they land: the weights are normalised straight out of the gather buffer
+    (mepol_iw_normalize_gathered), the gamma kernel reads dH/dW there through CSR row ids
+    remapped once per epoch to that layout, the entropy pass writes its sums into the block it
+    sends, the gradients are concatenated into a persistent flat buffer that is all-reduced in
+    place, and one launch (mepol_sharded_emit) forms the control scalars."""
 
     def __init__(self, tgt, optimizer, ep, G, B, ns, eps):
         super().__init__(tgt, optimizer, _LocalView(ep), ep.k, G, B, ns, eps)
@@ -352,12 +357,19 @@ class ShardedIteration(DeviceIteration):
         self.xs_all = torch.zeros(W, **f64)
         self.xu = torch.zeros(n + 1, **f64)
         self.xu_all = torch.zeros(W * (n + 1), **f64)
-        self.xg = torch.zeros(n + 2, **f64)
-        self.xg_all = torch.zeros(W * (n + 2), **f64)
-        self.u_glob = torch.zeros(self.N_global, **f64)
+        self.xg = torch.zeros(n + 4, **f64)               # [dH/dW | H, KL, H-sum, KL-sum]
+        self.xg_all = torch.zeros(W * (n + 4), **f64)     # dH/dW at theta_t of every particle
         self.w_glob = torch.zeros(self.N_global, **f64)   # importance weights at theta_t
-        self.g_glob = torch.zeros(self.N_global, **f64)   # dH/dW at theta_t, every particle
         self.sums_cur = torch.zeros(2, **f64)             # [H-sum, KL-sum] at theta_t
+        self.csr_rows_x = torch.empty_like(self.csr_rows)  # CSR ids in the xg_all layout
+        # flat gradient buffer (all-reduced in place) and its per-parameter views, in the
+        # optimizer's parameter order
+        sizes = [p.numel() for p in self.params]
+        self.flat_grad = torch.zeros(sum(sizes), **f64)
+        self.grad_views, o = [], 0
+        for p, sz in zip(self.params, sizes):
+            self.grad_views.append(self.flat_grad[o:o + sz].view_as(p))
+            o += sz
 
     def matches_epoch(self, tgt, optimizer, ep, G, B, ns, eps):
         return (self.matches(tgt, optimizer, _LocalView(ep), ep.k, G, B, ns, eps)
@@ -368,34 +380,36 @@ class ShardedIteration(DeviceIteration):
         self.ep = ep
         self.load(_LocalView(ep), logp_b)
 
+    def load(self, batch, logp_b=None):
+        super().load(batch, logp_b)
+        # global particle id j -> its dH/dW in xg_all: rank j // n, block stride n + 4
+        n, rows = self.N, self.csr_rows
+        torch.add(torch.div(rows, n, rounding_mode="floor") * (n + 4), torch.remainder(rows, n),
+                  out=self.csr_rows_x)
+
     def _gather_into(self, out, t):
         self.dist.all_gather_into_tensor(out, t, group=self.group)
 
     def _fwd_exchange(self):
-        """Weights, dH/dW and the [H-sum, KL-sum] of self.logp (the last forward) over all
-        ranks: collectives 3 and 4.  w_glob / g_glob are overwritten."""
+        """Weights, dH/dW and the raw entropy / KL sums of self.logp (the last forward) over all
+        ranks: collectives 3 and 4.  w_glob and xg_all are overwritten."""
         ops, n, W = self.ep.ops, self.N, self.world
         lt = self.logp.view(self.nt, self.T)
         _, ts, _, _ = ops.iw_forward(lt, self.logp_b, self.offsets, n, normalize=False,
                                      u_out=self.xu[:n])
         torch.sum(ts, 0, keepdim=True, out=self.xu[n:])
         self._gather_into(self.xu_all, self.xu)
-        xa = self.xu_all.view(W, n + 1)
-        U = xa[:, n].sum()                        # fixed-order sum of the per-rank normalisers
-        self.u_glob.view(W, n).copy_(xa[:, :n])
-        ops.iw_normalize(self.u_glob, U, out=self.w_glob)
-        out4, _, _ = ops.entropy_forward(self.w_glob, self.idx32T, self.D, self.k, self.ns,
-                                         self.G, self.B, self.eps, n_w=self.N_global,
-                                         g_out=self.xg[:n])
-        self.xg[n:].copy_(out4[2:4])
+        ops.iw_normalize_gathered(self.xu_all, W, n, self.w_glob)
+        ops.entropy_forward(self.w_glob, self.idx32T, self.D, self.k, self.ns, self.G, self.B,
+                            self.eps, n_w=self.N_global, g_out=self.xg[:n], out4=self.xg[n:])
         self._gather_into(self.xg_all, self.xg)
-        xg = self.xg_all.view(W, n + 2)
-        self.g_glob.view(W, n).copy_(xg[:, :n])
-        return xg[:, n:].sum(0)
 
     @torch.no_grad()
     def _prime(self):
-        self.sums_cur.copy_(self._fwd_exchange())
+        self._fwd_exchange()
+        # sums_cur <- the gathered sums (vals is rewritten by the next replay before it is read)
+        self.ep.ops.sharded_emit(self.xg_all, self.world, self.N + 4, self.N + 2, self.B,
+                                 self.N_global, self.sums_cur, self.vals)
 
     @torch.no_grad()
     def _body(self):
@@ -405,27 +419,25 @@ class ShardedIteration(DeviceIteration):
         # dH/dlogp at theta_t (_ShardedEntropy.backward) from the weights / dH/dW the previous
         # replay (or _prime) left
         w_local = self.w_glob[self.R0:self.R0 + n]
-        gamma, partials, nparts = ops.entropy_gamma(self.g_glob, w_local, self.csr_off,
-                                                    self.csr_rows)
+        gamma, partials, nparts = ops.entropy_gamma(self.xg_all, w_local, self.csr_off,
+                                                    self.csr_rows_x)
         torch.sum(partials[:nparts], 0, keepdim=True, out=self.xs)
         self._gather_into(self.xs_all, self.xs)
         S = self.xs_all.sum()
         grad = ops.entropy_reverse_scan(gamma, w_local, partials, nparts, self.offsets, nt, T,
                                         self.neg_one, S_ext=S)
-        dW1, db1, dW2, db2, dWm, dbm, dls = self._backward(grad.view(-1))
-        grad_of = {id(p): t for p, t in zip(self.named, (dW1, db1, dW2, db2, dWm, dbm, dls))}
-        flat = torch.cat([grad_of[id(p)].reshape(-1) for p in self.params])
-        self.dist.all_reduce(flat, group=self.group)  # ShardedEpoch.allreduce_grads
-        grads, o = [], 0
-        for p in self.params:
-            grads.append(flat[o:o + p.numel()].view_as(p))
-            o += p.numel()
-        self._optim_step(grads)
+        got = self._backward(grad.view(-1))
+        grad_of = {id(p): t for p, t in zip(self.named, got)}
+        torch.cat([grad_of[id(p)].reshape(-1) for p in self.params], out=self.flat_grad)
+        self.dist.all_reduce(self.flat_grad, group=self.group)  # ShardedEpoch.allreduce_grads
+        self._optim_step(self.grad_views)
         # KL at theta_t+1 (ShardedEpoch.compute_kl); H(theta_t+1) and dH/dW for the next replay
         self.forward()
-        sums = self._fwd_exchange()
-        torch.stack((self.B - self.sums_cur[0], sums[1] / self.N_global), out=self.vals)
-        self._emit(self.vals, 0, self.vals, 1, self.sums_cur, sums, 2)
+        self._fwd_exchange()
+        # vals = (H(theta_t), KL(theta_t+1)), sums_cur = theta_t+1's sums, vals to the host
+        ops.sharded_emit(self.xg_all, self.world, n + 4, n + 2, self.B, self.N_global,
+                         self.sums_cur, self.vals)
+        ops.memcpy_async(self.vals_host, self.vals)
 
     def step(self, speculate=False):
         H, KL = super().step(speculate)

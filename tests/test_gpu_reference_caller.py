@@ -93,7 +93,7 @@ def test_reference_shaped_epoch_matches_graph_loop(cuda, kl_threshold, lr):
     with torch.no_grad():
         h = M.compute_entropy(beh, beh, st, ac, nt, rl, D, I, k, G, B, ns, eps)
     assert h.device.type == "cpu" and h.dtype == torch.float64 and h.dim() == 0
-    assert ref["n"] >= 1
+    assert ref["n"] >= 1 or kl_threshold < 0.1  # the tight threshold may reject every step
 
     # the build's own loop (graph replay + speculation) on the same particles
     beh.load_state_dict(init)

@@ -3,7 +3,7 @@
 set -o pipefail
 out=gpurun_out/${1:-r4h}
 mkdir -p "$out"
-timeout -k 10 900 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_device_loop.py \
+timeout -k 10 900 python -u -m pytest tests/test_gpu_gemm.py tests/test_gpu_device_loop.py tests/test_gpu_sharded_graph.py tests/test_gpu_entropy.py \
   tests/test_gpu_policy.py tests/test_gpu_reference_caller.py -m gpu -v --timeout 600 \
   --timeout-method thread > "$out/tests.log" 2>&1 || { tail -60 "$out/tests.log"; exit 1; }
 tail -2 "$out/tests.log"

@@ -1,3 +1,10 @@
+// MEASURED AND DROPPED (round 4; not built into the product library).  The graph iteration with
+// this backward took 5.46 ms at C3 against 3.77 ms for head_bwd_kernel + rocBLAS dW2 + the dh1
+// kernel reading dz2 (profiles/r4/fused_head_dropped_timeline_C3.txt): dw2_kernel 2.22 ms (the
+// rocBLAS GEMM 1.0 ms), the dz2-forming dh1 variant 3.93 ms (1.93 ms reading dz2: the formation
+// sits between the MFMA block and the barrier of its single workgroup per CU), the record
+// reduction 153 us.  Kept as the starting point for a later attempt.
+//
 // Policy-head backward without the dz2 round trip (round 4).
 //
 // The reference's loss.backward() (src/algorithms/mepol.py:278) runs through
