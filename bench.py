@@ -157,11 +157,14 @@ class _EmulatedDist:
     def all_gather_into_tensor(self, out, inp, group=None):
         o = out.view(self.world, -1)
         flat = inp.reshape(-1)
-        o[0].copy_(flat)
         pe = self.peers  # ShardedEpoch gathers flattened tensors: match by size and dtype
-        src = pe if (pe and pe[0].numel() == inp.numel() and pe[0].dtype == inp.dtype) else None
+        if not (pe and pe[0].numel() == inp.numel() and pe[0].dtype == inp.dtype):
+            # one launch writing all world slots, as RCCL's one all_gather kernel does
+            o.copy_(flat.unsqueeze(0).expand(self.world, -1))
+            return
+        o[0].copy_(flat)
         for r in range(1, self.world):
-            o[r].copy_(src[r - 1].reshape(-1) if src is not None else flat)
+            o[r].copy_(pe[r - 1].reshape(-1))
 
     def all_reduce(self, t, op=None, group=None):
         return None

@@ -46,9 +46,12 @@ __device__ __forceinline__ bool nonfinite_bits(float v) {
   return (b & 0x7f800000u) == 0x7f800000u;
 }
 
+// out_bits2 (nullable): a second max slot fed from the same rows (queries == candidates: the
+// self k-NN of mepol.py:190-192 needs one pass, not two).
 __global__ __launch_bounds__(256) void norms_kernel(const float* __restrict__ X, int64_t n, int d,
                                                     unsigned* __restrict__ out_bits,
-                                                    unsigned* __restrict__ bad) {
+                                                    unsigned* __restrict__ bad,
+                                                    unsigned* __restrict__ out_bits2) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float nrm = 0.f;
   bool nonfinite = false, overflow = false;
@@ -64,7 +67,10 @@ __global__ __launch_bounds__(256) void norms_kernel(const float* __restrict__ X,
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) nrm = fmaxf(nrm, __shfl_xor(nrm, m, kWave));
-  if ((threadIdx.x & 63) == 0) atomicMax(out_bits, __float_as_uint(nrm));
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(out_bits, __float_as_uint(nrm));
+    if (out_bits2) atomicMax(out_bits2, __float_as_uint(nrm));
+  }
   const unsigned long long b1 = __ballot(nonfinite), b2 = __ballot(overflow);
   if ((threadIdx.x & 63) == 0) {
     if (b1) atomicAdd(bad, (unsigned)__popcll(b1));
@@ -851,10 +857,12 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
   MEPOL_HIP(hipMemsetAsync(ws + P.off_scalars, 0, 32, st));
   if (n_fallback_out) MEPOL_HIP(hipMemsetAsync(n_fallback_out, 0, sizeof(int32_t), st));
   // scal[0] = max candidate norm (refine's C), scal[2] = max query norm (f16 scale)
+  const bool self_query = query == cand && P.nq == P.nc;
   hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nc + 255) / 256)), dim3(256), 0, st, cand,
-                     P.nc, P.d, cmax, cmax + 4);
-  hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nq + 255) / 256)), dim3(256), 0, st, query,
-                     P.nq, P.d, cmax + 2, cmax + 4);
+                     P.nc, P.d, cmax, cmax + 4, self_query ? cmax + 2 : nullptr);
+  if (!self_query)
+    hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nq + 255) / 256)), dim3(256), 0, st, query,
+                       P.nq, P.d, cmax + 2, cmax + 4, nullptr);
   MEPOL_CHECK_LAUNCH();
   {
     // sklearn rejects non-finite input (ValueError from check_array): validate before the scan.
