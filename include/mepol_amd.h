@@ -12,8 +12,9 @@
  *    workspace whose size the *_workspace_size query returns.
  *  - `stream` is a hipStream_t; every call only enqueues work on it (no host sync), so calls
  *    can be captured into a hipGraph -- with ONE exception: mepol_knn synchronises `stream`
- *    once per call to validate its input before the scan (sklearn raises on NaN / inf), so it
- *    is never captured; the per-iteration entry points (entropy, IW, head, GEMMs, optimizer)
+ *    once per call to validate its input before the scan (sklearn raises on NaN / inf);
+ *    mepol_knn_deferred is the same call with the validation result left on the device, and
+ *    never blocks.  The per-iteration entry points (entropy, IW, head, GEMMs, optimizer)
  *    never synchronise.
  *  - Return value: 0 on success, a hipError_t value or one of the MEPOL_ERR_* codes otherwise;
  *    mepol_last_error_string() describes the last failure of the calling thread.
@@ -68,6 +69,15 @@ int mepol_knn_plan_info(int64_t n_cand, int64_t n_query, int d, int kp1, int spl
 int mepol_knn(const float* cand, int64_t n_cand, const float* query, int64_t n_query, int d,
               int kp1, int split_hint, double* dist_out, int64_t* idx_out, int32_t* idx32_out,
               int32_t* n_fallback_out, void* workspace, size_t workspace_bytes, void* stream);
+/* mepol_knn without the host synchronisation: invalid_out (device int32 [2], required) receives
+ * [rows with a NaN / inf coordinate, rows whose squared norm overflows f32] in stream order,
+ * and when either is nonzero every later kernel of the call returns at once (the outputs are
+ * then undefined).  The caller reads invalid_out at its next synchronisation point and raises
+ * as mepol_knn would; the epoch path does so once the CSR build is queued behind the k-NN. */
+int mepol_knn_deferred(const float* cand, int64_t n_cand, const float* query, int64_t n_query,
+                       int d, int kp1, int split_hint, double* dist_out, int64_t* idx_out,
+                       int32_t* idx32_out, int32_t* n_fallback_out, int32_t* invalid_out,
+                       void* workspace, size_t workspace_bytes, void* stream);
 /* Exhaustive f64 scan for every query (kp1 <= 64); scratch_idx: int32 [1 + n_query]. */
 int mepol_knn_exact(const float* cand, int64_t n_cand, const float* query, int64_t n_query, int d,
                     int kp1, double* dist_out, int64_t* idx_out, int32_t* idx32_out,

@@ -27,6 +27,8 @@ SIGNATURES = {
                             ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)],
     "mepol_knn": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                   _c_vp, _c_sz, _c_vp],
+    "mepol_knn_deferred": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_int, _c_vp, _c_vp,
+                           _c_vp, _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_knn_exact": [_c_vp, _c_i64, _c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_vp,
                         _c_vp],
     "mepol_iw_forward": [_c_vp, _c_vp, _c_i64, _c_i64, _c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp,

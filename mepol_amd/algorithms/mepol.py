@@ -290,7 +290,8 @@ def collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len
                                         "that can be equally split among workers"
     s32, a32, rtl32, ns32 = collect_particles_device(env, behavioral_policy, num_traj, traj_len,
                                                      state_filter)
-    D, I, I32T = ops.knn(ns32, k + 1)
+    # the k-NN's input check is read once the work behind it is queued (mepol_knn_deferred)
+    D, I, I32T, check = ops.knn(ns32, k + 1, defer_check=True)
     states = s32.to(float_type)
     actions = a32.to(float_type)
     next_states = ns32.to(float_type)
@@ -298,16 +299,18 @@ def collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len
     batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T)
     P.register(I, batch)
     batch.csr(k)  # queued now: the GPU builds it while the host sets up the off-policy loop
+    check.raise_if_invalid()  # sklearn's check_array ValueError, as kneighbors raises it
     return states, actions, real_traj_lengths, next_states, D, I
 
 
 def make_particle_batch(states, actions, real_traj_lengths, next_states_f32, k):
     """Register a batch built from externally produced particles (e.g. a MuJoCo rollout or a
     synthetic benchmark batch): runs the GPU k-NN and returns the reference's 6-tuple."""
-    D, I, I32T = ops.knn(next_states_f32, k + 1)
+    D, I, I32T, check = ops.knn(next_states_f32, k + 1, defer_check=True)
     batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T)
     P.register(I, batch)
     batch.csr(k)  # queued now: the GPU builds it while the host sets up the off-policy loop
+    check.raise_if_invalid()
     return states, actions, real_traj_lengths, next_states_f32.to(float_type), D, I
 
 

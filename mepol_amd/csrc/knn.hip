@@ -46,36 +46,92 @@ __device__ __forceinline__ bool nonfinite_bits(float v) {
   return (b & 0x7f800000u) == 0x7f800000u;
 }
 
+// Row blocks of the norms / pack kernels: the rows are read into LDS as one contiguous span
+// (one coalesced 256-B access per wave-instruction; a row per lane read straight from HBM would
+// touch 64 lines per instruction, d-float stride) and used from there.
+constexpr int kStageRows = 128;
+
+// kStageRows rows of X (d floats each) into sx, coalesced, kStageBatch loads in flight per
+// thread (a plain copy loop waits for each load before its LDS store).  Returns the rows present.
+constexpr int kStageBatch = 8;
+__device__ __forceinline__ int stage_rows(const float* __restrict__ X, int64_t n, int d, int64_t r0,
+                                          float* sx) {
+  const int rows = (int)min<int64_t>(kStageRows, n - r0);
+  const int cnt = rows * d;
+  const float* src = X + r0 * d;
+  const int nt = blockDim.x;
+  for (int e0 = threadIdx.x; e0 < cnt; e0 += kStageBatch * nt) {
+    float v[kStageBatch];
+#pragma unroll
+    for (int u = 0; u < kStageBatch; ++u) v[u] = src[min(e0 + u * nt, cnt - 1)];
+#pragma unroll
+    for (int u = 0; u < kStageBatch; ++u)
+      if (e0 + u * nt < cnt) sx[e0 + u * nt] = v[u];
+  }
+  __syncthreads();
+  return rows;
+}
+
 // out_bits2 (nullable): a second max slot fed from the same rows (queries == candidates: the
-// self k-NN of mepol.py:190-192 needs one pass, not two).
-__global__ __launch_bounds__(256) void norms_kernel(const float* __restrict__ X, int64_t n, int d,
-                                                    unsigned* __restrict__ out_bits,
-                                                    unsigned* __restrict__ bad,
-                                                    unsigned* __restrict__ out_bits2) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// self k-NN of mepol.py:190-192 needs one pass, not two).  Launched with 256 threads per block
+// (all of them stage rows; threads < kStageRows then reduce one row each; grid-stride over row
+// blocks) and kStageRows * d floats of dynamic LDS.  One atomic per block and slot, and few
+// blocks: the max lands on one address from every block, and those device-scope atomics
+// serialise (1563 blocks took ~42 us at 200k rows, where staging the rows takes ~10).
+constexpr int kNormsBlocks = 256;
+constexpr int kNormsThreads = 256;
+__global__ __launch_bounds__(kNormsThreads) void norms_kernel(const float* __restrict__ X, int64_t n,
+                                                           int d, unsigned* __restrict__ out_bits,
+                                                           unsigned* __restrict__ bad,
+                                                           unsigned* __restrict__ out_bits2) {
+  extern __shared__ float sx[];
+  __shared__ float s_nrm[kNormsThreads / 64];
+  __shared__ unsigned s_bad[2];
+  if (threadIdx.x == 0) s_bad[0] = s_bad[1] = 0u;
   float nrm = 0.f;
-  bool nonfinite = false, overflow = false;
-  if (i < n) {
-    const float* x = X + i * d;
-    float s2 = 0.f;
-    for (int f = 0; f < d; ++f) {
-      nonfinite |= nonfinite_bits(x[f]);
-      s2 = fmaf(x[f], x[f], s2);
+  unsigned nonfinite_rows = 0, overflow_rows = 0;
+  for (int64_t r0 = (int64_t)blockIdx.x * kStageRows; r0 < n; r0 += (int64_t)gridDim.x * kStageRows) {
+    __syncthreads();  // the previous step's LDS reads are done
+    const int rows = stage_rows(X, n, d, r0, sx);
+    if ((int)threadIdx.x < rows) {
+      const float* x = sx + threadIdx.x * d;
+      float s2 = 0.f;
+      unsigned mag = 0;  // max |x_f| bit pattern: integer ops, no float compare to fold
+      for (int f = 0; f < d; ++f) {
+        const float v = x[f];
+        mag = max(mag, __float_as_uint(v) & 0x7fffffffu);
+        s2 = fmaf(v, v, s2);
+      }
+      const bool nonfinite = nonfinite_bits(__uint_as_float(mag));
+      const bool overflow = !nonfinite && nonfinite_bits(s2);
+      nonfinite_rows += nonfinite;
+      overflow_rows += overflow;
+      if (!nonfinite && !overflow) nrm = fmaxf(nrm, sqrtf(s2));
     }
-    overflow = !nonfinite && nonfinite_bits(s2);
-    nrm = (nonfinite || overflow) ? 0.f : sqrtf(s2);
   }
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) nrm = fmaxf(nrm, __shfl_xor(nrm, m, kWave));
-  if ((threadIdx.x & 63) == 0) {
-    atomicMax(out_bits, __float_as_uint(nrm));
-    if (out_bits2) atomicMax(out_bits2, __float_as_uint(nrm));
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) s_nrm[w] = nrm;
+  __syncthreads();
+  if (nonfinite_rows) atomicAdd(&s_bad[0], nonfinite_rows);
+  if (overflow_rows) atomicAdd(&s_bad[1], overflow_rows);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = s_nrm[0];
+    for (int i = 1; i < kNormsThreads / 64; ++i) m = fmaxf(m, s_nrm[i]);
+    atomicMax(out_bits, __float_as_uint(m));
+    if (out_bits2) atomicMax(out_bits2, __float_as_uint(m));
+    if (s_bad[0]) atomicAdd(bad, s_bad[0]);
+    if (s_bad[1]) atomicAdd(bad + 1, s_bad[1]);
   }
-  const unsigned long long b1 = __ballot(nonfinite), b2 = __ballot(overflow);
-  if ((threadIdx.x & 63) == 0) {
-    if (b1) atomicAdd(bad, (unsigned)__popcll(b1));
-    if (b2) atomicAdd(bad + 1, (unsigned)__popcll(b2));
-  }
+}
+
+// Rejected input (non-finite rows, squared norms beyond f32): norms_kernel counted them into
+// scal[4..5].  The deferred entry point does not stop the stream to look, so every later kernel
+// of the call checks and does nothing (its outputs are then undefined, the caller raises).
+__device__ __forceinline__ bool input_rejected(const unsigned* __restrict__ scal) {
+  return (scal[4] | scal[5]) != 0u;
 }
 
 // apack16[((t*64 + l)*KS16 + s)*16 + {0..7 hi, 8..15 lo}] = A[i = l&31][k = 16 s + 8 (l>>5) + j]
@@ -91,34 +147,37 @@ __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X
                                                      _Float16* __restrict__ apack,
                                                      const unsigned* __restrict__ scal,
                                                      float* __restrict__ cpad, int dp) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (gid >= nct * 64) return;
+  // 4 tiles (kStageRows = 128 candidates) per block of 256 threads, staged through LDS
+  extern __shared__ float sx[];
+  if (input_rejected(scal)) return;  // block-uniform, before the barrier
+  const int64_t c0 = (int64_t)blockIdx.x * kStageRows;
+  const int rows = stage_rows(X, n, d, c0, sx);
+  // cpad rows of this block: one contiguous span, written with dwordx4 in order
+  {
+    f32x4* dst = reinterpret_cast<f32x4*>(cpad + c0 * dp);
+    const int nv = rows * dp / 4;
+    for (int e = threadIdx.x; e < nv; e += blockDim.x) {
+      const int r = (4 * e) / dp, f0 = (4 * e) % dp;
+      f32x4 v;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = f0 + u < d ? sx[r * d + f0 + u] : 0.f;
+      dst[e] = v;
+    }
+  }
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= nct) return;
   const float sg = knn_scale(scal);
-  const int64_t t = gid >> 6;
-  const int l = (int)(gid & 63);
+  const int l = threadIdx.x & 63;
   const int h = l >> 5;
-  const int64_t c = t * 32 + (l & 31);
-  const bool valid = c < n;
+  const int lr = (threadIdx.x >> 6) * 32 + (l & 31);  // row within the block
+  const bool valid = lr < rows;
+  const float* xc = sx + lr * d;
   float cn = 0.f;
-  if (valid) {
-    const float* xc = X + c * d;
+  if (valid)
     for (int f = 0; f < d; ++f) {
       const float y = sg * xc[f];
       cn = fmaf(y, y, cn);
     }
-    // this thread's half of the padded row
-    const int half = dp / 2;
-    f32x4* dst = reinterpret_cast<f32x4*>(cpad + c * dp + h * half);
-    for (int f4 = 0; f4 < half / 4; ++f4) {
-      f32x4 v;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int f = h * half + 4 * f4 + u;
-        v[u] = f < d ? xc[f] : 0.f;
-      }
-      dst[f4] = v;
-    }
-  }
   for (int s = 0; s < KS16; ++s) {
     f16x8 hv, lv;
 #pragma unroll
@@ -126,7 +185,7 @@ __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X
       const int f = 16 * s + 8 * h + j;
       float v;
       if (valid)
-        v = (f < d) ? -2.f * sg * X[c * d + f] : ((f == d) ? cn : 0.f);
+        v = (f < d) ? -2.f * sg * xc[f] : ((f == d) ? cn : 0.f);
       else
         v = (f == d) ? kPadNorm16 : 0.f;
       _Float16 a, b;
@@ -237,7 +296,7 @@ __global__ __launch_bounds__(256) void refine_kernel(
   const int64_t xcd = bx & 7, per = nb >> 3, rem = nb & 7;
   const int64_t qb = xcd * per + min(xcd, rem) + (bx >> 3);
   const int64_t q = qb * 4 + w;
-  if (q >= nq) return;
+  if (q >= nq || input_rejected(cmax_bits)) return;
   // Candidate entries of this query: 2*split ascending partial lists of list_len each, the last
   // slot of each carrying that lane's prune bound (select16_kernel).
   const float* lv = lists_v + q * M;
@@ -281,13 +340,38 @@ __global__ __launch_bounds__(256) void refine_kernel(
 #pragma unroll
     for (int p = 0; p < MAXP; ++p) rk[p] = 0;
     const int mtot = min(nval, 64 * kRM);
+    if (rank_merge == 2) {
+      // Each of the 2 split partial lists is ascending in value: an entry's rank is, per list,
+      // a binary search for the entries of smaller value plus the (rare) equal-value entries of
+      // smaller index -- O(lists x log LIST16) LDS reads per entry instead of all M.
+      const int nl = mtot / list_len;
+      const float2* se = sent[w];
 #pragma nounroll
-    for (int e = 0; e < mtot; ++e) {
-      const float2 o = sent[w][e];
-      const float ov = o.x;
-      const int oi = __float_as_int(o.y);
+      for (int s = 0; s < nl; ++s) {
+        const float2* L = se + s * list_len;
 #pragma unroll
-      for (int p = 0; p < MAXP; ++p) rk[p] += lex_less_f(ov, oi, ev[p], ei[p]) ? 1 : 0;
+        for (int p = 0; p < MAXP; ++p) {
+          int k = 0;
+#pragma unroll
+          for (int step = 32; step >= 1; step >>= 1)
+            if (k + step <= list_len && L[k + step - 1].x < ev[p]) k += step;
+          int c = k;
+          while (ei[p] != INT_MAX && k < list_len && L[k].x == ev[p]) {
+            c += __float_as_int(L[k].y) < ei[p] ? 1 : 0;
+            ++k;
+          }
+          rk[p] += c;
+        }
+      }
+    } else {
+#pragma nounroll
+      for (int e = 0; e < mtot; ++e) {
+        const float2 o = sent[w][e];
+        const float ov = o.x;
+        const int oi = __float_as_int(o.y);
+#pragma unroll
+        for (int p = 0; p < MAXP; ++p) rk[p] += lex_less_f(ov, oi, ev[p], ei[p]) ? 1 : 0;
+      }
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -623,7 +707,7 @@ struct Plan {
   int LIST16;     // per-half select list length
   int M;          // refine input entries per query: 2*split*LIST16
   int64_t nc, nq, nct, nqt, tiles_per_split;
-  size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_part, off_cpad, total;
+  size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_part, off_cpad, off_seed, total;
 };
 
 static const int kListChoices[] = {8, 16, 24, 32, 40};
@@ -684,6 +768,12 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   // operand splitting 3 * 2^-22 = 12 * 2^-24, |c|^2 in f32 (d), x2.
   P->e_terms = P->nh == 1 ? 8192 + 64 + 2 * (2 * 16 * P->KS16 + 16 + d)
                           : 2 * (3 * 16 * P->KS16 + 16 + d);
+  // Candidate-hi plans with <= 3 k-steps (d <= 47) drop the query's lo half too
+  // (select16_kernel: kQueryLo): its f16 rounding, 2^-11 2 |c||q| (+64 for subnormals), joins
+  // the bound.  Measured C3 7.0 -> 5.7 ms, d = 47 9.9 -> 8.0 ms with no added fallbacks; at d = 63,
+  // k+1 = 51 (C5) the wider band sent 1633 of 500k queries to the exhaustive path (8 with it),
+  // so 4-step plans keep it (profiles/r4/knn/qlo_ab_probe.log).
+  if (P->nh == 1 && P->KS16 <= 3) P->e_terms += 8192 + 64;
   // the selection's error band (~0.1 at C3) holds a few more candidates around the (k+1)-th
   // than kp1 + 4: refine ranks the approximate top 64 and evaluates those inside the band
   P->LIST = kRefineList;
@@ -733,15 +823,27 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   P->dp = (d + 31) / 32 * 32;
   P->off_cpad = off;
   off = align_up(off + (size_t)nc * P->dp * sizeof(float), 256);
+  P->off_seed = off;  // per-query prune-bound seeds (select16_kernel)
+  off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(int), 256);
   P->total = off;
   return 0;
 }
 
-// MEPOL_KNN_RANK_MERGE=0 selects the argmin-round merge in refine_kernel (A/B probe).
+// MEPOL_KNN_SEED=0: every candidate range starts its prune bound at +inf (A/B probe).
+static int select_seed() {
+  static const int v = [] {
+    const char* e = getenv("MEPOL_KNN_SEED");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
+
+// refine_kernel's merge of the partial lists: 2 = per-list binary-search ranks (default),
+// 1 = ranks counted against every entry, 0 = argmin rounds (MEPOL_KNN_RANK_MERGE, A/B probe).
 static int refine_rank_merge() {
   static const int v = [] {
     const char* e = getenv("MEPOL_KNN_RANK_MERGE");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }
@@ -827,10 +929,13 @@ extern "C" int mepol_knn_plan_info(int64_t n_cand, int64_t n_query, int d, int k
   return 0;
 }
 
-extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, int64_t n_query,
-                         int d, int kp1, int split_hint, double* dist_out, int64_t* idx_out,
-                         int32_t* idx32_out, int32_t* n_fallback_out, void* workspace,
-                         size_t workspace_bytes, void* stream) {
+// invalid_out == nullptr: validate on the host (one stream synchronisation after the norms pass,
+// like the reference's blocking kneighbors).  Otherwise the two counts go to invalid_out on the
+// device and the call never blocks (mepol_knn_deferred).
+static int knn_impl(const float* cand, int64_t n_cand, const float* query, int64_t n_query, int d,
+                    int kp1, int split_hint, double* dist_out, int64_t* idx_out,
+                    int32_t* idx32_out, int32_t* n_fallback_out, int32_t* invalid_out,
+                    void* workspace, size_t workspace_bytes, void* stream) {
   Plan P;
   int rc = make_plan(n_cand, n_query, d, kp1, split_hint, &P);
   if (rc) return rc;
@@ -858,15 +963,21 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
   if (n_fallback_out) MEPOL_HIP(hipMemsetAsync(n_fallback_out, 0, sizeof(int32_t), st));
   // scal[0] = max candidate norm (refine's C), scal[2] = max query norm (f16 scale)
   const bool self_query = query == cand && P.nq == P.nc;
-  hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nc + 255) / 256)), dim3(256), 0, st, cand,
+  const size_t stage_lds = (size_t)kStageRows * P.d * sizeof(float);  // <= 32 KB (d <= 63)
+  auto norms_grid = [](int64_t rows) {
+    return dim3((unsigned)std::min<int64_t>(kNormsBlocks, (rows + kStageRows - 1) / kStageRows));
+  };
+  hipLaunchKernelGGL(norms_kernel, norms_grid(P.nc), dim3(kNormsThreads), stage_lds, st, cand,
                      P.nc, P.d, cmax, cmax + 4, self_query ? cmax + 2 : nullptr);
   if (!self_query)
-    hipLaunchKernelGGL(norms_kernel, dim3((unsigned)((P.nq + 255) / 256)), dim3(256), 0, st, query,
+    hipLaunchKernelGGL(norms_kernel, norms_grid(P.nq), dim3(kNormsThreads), stage_lds, st, query,
                        P.nq, P.d, cmax + 2, cmax + 4, nullptr);
   MEPOL_CHECK_LAUNCH();
-  {
+  if (invalid_out) {
+    MEPOL_HIP(hipMemcpyAsync(invalid_out, cmax + 4, 2 * sizeof(int32_t), hipMemcpyDeviceToDevice,
+                             st));
+  } else {
     // sklearn rejects non-finite input (ValueError from check_array): validate before the scan.
-    // One stream synchronisation per call, like the reference's blocking kneighbors.
     unsigned bad[2] = {0, 0};
     MEPOL_HIP(hipMemcpyAsync(bad, cmax + 4, sizeof(bad), hipMemcpyDeviceToHost, st));
     MEPOL_HIP(hipStreamSynchronize(st));
@@ -879,13 +990,17 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
       return kErrUnsupported;
     }
   }
-  const int64_t total = P.nct * 64;
-  hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, cand,
-                     P.nc, P.d, P.KS16, P.nh, P.nct, ap16, cmax, cpad, P.dp);
+  hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((P.nct + 3) / 4)), dim3(256), stage_lds, st,
+                     cand, P.nc, P.d, P.KS16, P.nh, P.nct, ap16, cmax, cpad, P.dp);
   MEPOL_CHECK_LAUNCH();
   {
+    int* seed = nullptr;
+    if (P.split > 1 && select_seed()) {
+      seed = (int*)(ws + P.off_seed);
+      MEPOL_HIP(hipMemsetD32Async((hipDeviceptr_t)seed, kSeedNone, (size_t)P.nq, st));
+    }
     const SelectArgs sa{ap16,        query,  P.nq,   P.d,    P.nct, P.split, P.tiles_per_split,
-                        P.keep,      P.LIST16, P.nh, P.nqt,  cmax,  lv,      li};
+                        P.keep,      P.LIST16, P.nh, P.nqt,  cmax,  lv,      li, seed};
     switch (P.KS16) {
       case 1: launch_select<1>(sa, st); break;
       case 2: launch_select<2>(sa, st); break;
@@ -900,6 +1015,27 @@ extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, 
                    pd, pi);
   MEPOL_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int mepol_knn(const float* cand, int64_t n_cand, const float* query, int64_t n_query,
+                         int d, int kp1, int split_hint, double* dist_out, int64_t* idx_out,
+                         int32_t* idx32_out, int32_t* n_fallback_out, void* workspace,
+                         size_t workspace_bytes, void* stream) {
+  return knn_impl(cand, n_cand, query, n_query, d, kp1, split_hint, dist_out, idx_out, idx32_out,
+                  n_fallback_out, nullptr, workspace, workspace_bytes, stream);
+}
+
+extern "C" int mepol_knn_deferred(const float* cand, int64_t n_cand, const float* query,
+                                  int64_t n_query, int d, int kp1, int split_hint,
+                                  double* dist_out, int64_t* idx_out, int32_t* idx32_out,
+                                  int32_t* n_fallback_out, int32_t* invalid_out, void* workspace,
+                                  size_t workspace_bytes, void* stream) {
+  if (!invalid_out) {
+    set_error("mepol_knn_deferred: null invalid_out");
+    return kErrBadArg;
+  }
+  return knn_impl(cand, n_cand, query, n_query, d, kp1, split_hint, dist_out, idx_out, idx32_out,
+                  n_fallback_out, invalid_out, workspace, workspace_bytes, stream);
 }
 
 // Exhaustive exact k-NN for every query (no f16 selection): the reference semantics at the

@@ -17,6 +17,7 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
 
+
 constexpr int kBufCap = 24;        // per-lane LDS insertion buffer (entries)
 constexpr int kMaxSplit = 16;
 constexpr int kExactGrid = 512;    // blocks of the exhaustive fallback (exact_kernel)
@@ -59,16 +60,21 @@ __device__ __forceinline__ void flush_buffer(float (&ld)[LIST], int (&li)[LIST],
                                              const float (*bv)[64], const int (*bi)[64], int l,
                                              float thr0, int keep = 0) {
   const int mc = wave_max_i(cnt);
+  // entry e + 1 is read from LDS while entry e is inserted (the read latency would otherwise
+  // sit in front of every insertion)
+  float x = bv[0][l];
+  int xi = bi[0][l];
 #pragma nounroll
   for (int e = 0; e < mc; ++e) {
-    if (e < cnt) {
-      const float x = bv[e][l];
-      const int xi = bi[e][l];
-      if (x < thr) {
-        list_insert<LIST>(ld, li, x, xi);
-        thr = ld[LIST - 1];
-      }
+    const int en = min(e + 1, kBufCap - 1);
+    const float xn = bv[en][l];
+    const int xin = bi[en][l];
+    if (e < cnt && x < thr) {
+      list_insert<LIST>(ld, li, x, xi);
+      thr = ld[LIST - 1];
     }
+    x = xn;
+    xi = xin;
   }
   cnt = 0;
   // lanes l and l^32 serve the same query: the tighter of their maxima is a valid prune bound
@@ -118,7 +124,19 @@ struct SelectArgs {
   const unsigned* scal;
   float* out_v;
   int* out_i;
+  int* seed;  // [nq] ordered keys of the per-query prune bounds the ranges publish (nullable)
 };
+
+// Order-preserving map of a float to an int (atomicMin on the int orders like the float; the
+// selection values are |c|^2 - 2 c.q, which can be negative).
+__device__ __forceinline__ int float_order_key(float v) {
+  const int b = __float_as_int(v);
+  return b >= 0 ? b : b ^ 0x7fffffff;
+}
+__device__ __forceinline__ float order_key_float(int k) {
+  return __int_as_float(k >= 0 ? k : k ^ 0x7fffffff);
+}
+constexpr int kSeedNone = 0x7f800000;  // float_order_key(+inf)
 
 // knn_select_ks<KS16>.hip
 template <int KS16>

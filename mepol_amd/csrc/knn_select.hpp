@@ -10,8 +10,10 @@ namespace knn {
 // f16 hi + lo (2^-22 relative).  NH = 1 (candidate-hi, the default): the candidates are the f16
 // hi halves of A and 2 MFMAs per k-step (A_hi q_hi + A_hi q_lo) accumulate in f32; the value's
 // error is dominated by the candidate rounding, 2^-11 (|c|^2 + 2 |c||q|), and only the hi half
-// travels (1 KB per k-step and tile).  NH = 2 (split candidates): A_hi and A_lo travel and 3
-// MFMAs per k-step (+ A_lo q_hi) give ~f32-class values, 2 (3 K + 16 + d) 2^-24 (|c|^2 + 2 |c||q|),
+// travels (1 KB per k-step and tile).  With <= 3 k-steps the q_lo MFMA is dropped as well (one
+// MFMA per k-step; the query rounding, 2^-11 2 |c||q|, joins the bound: make_plan).  NH = 2
+// (split candidates): A_hi and A_lo travel and 3 MFMAs per k-step (+ A_lo q_hi) give
+// ~f32-class values, 2 (3 K + 16 + d) 2^-24 (|c|^2 + 2 |c||q|),
 // for data whose neighbour spacing is below the f16 band (make_plan).  refine's certification
 // uses the plan's bound either way.
 // OCC = 3: __launch_bounds__(256, 3) caps the kernel at 168 VGPRs (3 waves per SIMD) for the
@@ -23,7 +25,8 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
                                                        int64_t tiles_per_split, int keep,
                                                        const unsigned* __restrict__ scal,
                                                        float* __restrict__ out_v,
-                                                       int* __restrict__ out_i) {
+                                                       int* __restrict__ out_i,
+                                                       int* __restrict__ seed) {
   __shared__ float sbuf_v[4][kBufCap][64];
   __shared__ int sbuf_i[4][kBufCap][64];
   const int w = threadIdx.x >> 6;
@@ -36,7 +39,7 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
   const bool xcd_map = (split & 7) == 0;
   const int sp = xcd_map ? (int)(lin % split) : (int)blockIdx.y;
   const int64_t qt = (xcd_map ? lin / split : (int64_t)blockIdx.x) * 4 + w;
-  if (qt * 32 >= nq) return;  // wave-uniform
+  if (qt * 32 >= nq || (scal[4] | scal[5])) return;  // wave-uniform (rejected input: knn.hip)
   const int h = l >> 5;
   const int64_t q = qt * 32 + (l & 31);
   const bool qvalid = q < nq;
@@ -75,7 +78,17 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
     ld[j] = INFINITY;
     li[j] = -1;
   }
-  const float thr0 = INFINITY;
+  // Seed of the prune bound: the tightest bound a range of this query already finished with
+  // (the grid runs split-major, so range 0's blocks are mostly done when range 1's start).  Any
+  // value is sound -- a lane only claims what its own scan rejected against its own bound, and
+  // refine certifies against the reported bounds -- and every published bound has >= 2 keep
+  // candidates of its range at or below it, so it costs no certification.  It skips most of the
+  // list warm-up, where the bulk of the insertions happen.  System scope: the load and the
+  // publishing atomic below go past the XCD's own (non-coherent) L2.
+  float thr0 = INFINITY;
+  if (seed && qvalid)
+    thr0 = order_key_float(
+        __hip_atomic_load(seed + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
   float thr = thr0;
   int cnt = 0;
 
@@ -89,6 +102,8 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
   // would otherwise reach the 256-VGPR cap (at the cap the asm-load buffers are not safe from
   // register copies).
   constexpr int NV = NH * KS16;  // dwordx4 per lane per tile: one per (k-step, half)
+  // query lo half: split-candidate plans and 4-k-step plans (make_plan's bound covers the rest)
+  constexpr bool kQueryLo = NH == 2 || KS16 >= 4;
   constexpr int NB = NH == 2 ? (KS16 >= 4 ? 2 : 3) : ((KS16 >= 4 && LIST > 32) ? 2 : 3);
   const f32x4* abase = reinterpret_cast<const f32x4*>(apack) + l;
   f32x4 Bf[NB][NV];
@@ -116,7 +131,8 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
     for (int s = 0; s < KS16; ++s) {
       const f16x8 ah = __builtin_bit_cast(f16x8, A[NH * s]);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bhi[s], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, blo[s], acc, 0, 0, 0);
+      if constexpr (kQueryLo)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, blo[s], acc, 0, 0, 0);
       if constexpr (NH == 2) {
         const f16x8 al = __builtin_bit_cast(f16x8, A[2 * s + 1]);
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bhi[s], acc, 0, 0, 0);
@@ -244,6 +260,10 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
     process(accP, t - 1);
   }
   flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0, keep);
+  // publish this range's final bound (the same in both lanes of the query)
+  if (seed && qvalid && h == 0)
+    __hip_atomic_fetch_min(seed + q, float_order_key(thr), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 
   if (qvalid) {
     // The last slot carries this lane's final bound: every candidate of its range that is not
@@ -276,7 +296,7 @@ static void launch_select16_gate(const SelectArgs& a, hipStream_t st) {
 #define MEPOL_SEL16O(L, O)                                                                        \
   hipLaunchKernelGGL((select16_kernel<KS16, L, NH, O, GATE>), g, dim3(256), 0, st, a.apack,      \
                      a.query, a.nq, a.d, a.nct, a.split, a.tiles_per_split, a.keep, a.scal, a.out_v,       \
-                     a.out_i)
+                     a.out_i, a.seed)
 #define MEPOL_SEL16(L) MEPOL_SEL16O(L, 1)
   switch (a.LIST16) {  // >= keep + 4 >= 7; split-candidate plans keep the instances that fit
     case 8: MEPOL_SEL16(8); break;

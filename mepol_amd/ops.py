@@ -80,11 +80,38 @@ def knn_plan(n_cand, n_query, d, kp1, split=0):
     return {"KS16": ks.value // 10, "nh": ks.value % 10, "LIST16": lst.value, "split": sp.value}
 
 
-def knn(cand, kp1, query=None, split=0, want_int64=True, return_fallback=False):
+class KnnInputCheck:
+    """The input validation of a deferred k-NN call (mepol_knn_deferred): the two counts stay
+    on the device, copied to pinned host memory in stream order; raise_if_invalid() waits for
+    that copy only and raises what mepol_knn would have raised."""
+
+    def __init__(self, invalid_dev):
+        self._host = torch.empty(2, dtype=torch.int32, pin_memory=True)
+        memcpy_async(self._host, invalid_dev)
+        self._event = torch.cuda.Event()
+        self._event.record(torch.cuda.current_stream(invalid_dev.device))
+        self._dev = invalid_dev
+
+    def raise_if_invalid(self):
+        from ._lib import MepolError, MepolInputError
+
+        self._event.synchronize()
+        nonfinite, overflow = (int(x) for x in self._host.tolist())
+        if nonfinite:
+            raise MepolInputError(f"mepol_knn failed (rc=1001): mepol_knn: Input contains NaN or "
+                                  f"infinity ({nonfinite} rows)")
+        if overflow:
+            raise MepolError(f"mepol_knn failed (rc=1003): mepol_knn: {overflow} rows have a "
+                             "squared norm beyond float32 range")
+
+
+def knn(cand, kp1, query=None, split=0, want_int64=True, return_fallback=False, defer_check=False):
     """Exact k-NN of `query` rows among `cand` rows (both f32 [*, d] on device).
 
     Returns (D f64 [nq, kp1], I int64 [nq, kp1] or None, I32T int32 [kp1, nq]) and, with
     return_fallback, the device int32 count of queries that took the exhaustive path.
+    defer_check: no host synchronisation inside the call (mepol_knn_deferred); a KnnInputCheck
+    is appended to the result and the caller must call its raise_if_invalid() before using it.
     Replaces NearestNeighbors(k+1).fit(X).kneighbors(X) (src/algorithms/mepol.py:190-192).
     """
     import ctypes
@@ -106,11 +133,15 @@ def knn(cand, kp1, query=None, split=0, want_int64=True, return_fallback=False):
     I = torch.empty((nq, kp1), dtype=torch.int64, device=dev) if want_int64 else None
     I32T = torch.empty((kp1, nq), dtype=torch.int32, device=dev)
     nfb = torch.zeros(1, dtype=torch.int32, device=dev)
+    out = (D, I, I32T) + ((nfb,) if return_fallback else ())
+    if defer_check:
+        invalid = torch.empty(2, dtype=torch.int32, device=dev)
+        call("mepol_knn_deferred", ptr(cand), nc, ptr(query), nq, d, kp1, split, ptr(D), ptr(I),
+             ptr(I32T), ptr(nfb), ptr(invalid), ptr(ws), ws.numel(), _stream())
+        return out + (KnnInputCheck(invalid),)
     call("mepol_knn", ptr(cand), nc, ptr(query), nq, d, kp1, split, ptr(D), ptr(I), ptr(I32T),
          ptr(nfb), ptr(ws), ws.numel(), _stream())
-    if return_fallback:
-        return D, I, I32T, nfb
-    return D, I, I32T
+    return out
 
 
 def knn_exact(cand, kp1, query=None, want_int64=True):

@@ -106,7 +106,12 @@ class ShardedEpoch:
     # -- per-epoch setup ------------------------------------------------------------------------
     def build_knn(self):
         cand = self._gather(self.next_states).reshape(self.N, -1)
-        self.D, self.I, self.idx32T = self.ops.knn(cand, self.k + 1, query=self.next_states)
+        self.D, self.I, self.idx32T, check = self.ops.knn(cand, self.k + 1,
+                                                          query=self.next_states,
+                                                          defer_check=True)
+        # rejected input on any rank: every rank's k-NN kernels returned early, and the
+        # gathered idx rows below are undefined, so each rank raises before using them
+        check.raise_if_invalid()
         idx_all = self._gather(self.idx32T[: self.k].contiguous())       # [G, k, n_local]
         idx_allT = idx_all.permute(1, 0, 2).reshape(self.k, self.N).contiguous()
         self.csr = self.ops.csr_build(idx_allT, self.k, self.n_local, col_offset=self.R0,

@@ -157,6 +157,41 @@ def test_knn_rejects_non_finite(cuda, bad, where):
     assert np.array_equal(D.cpu().numpy(), Do) and np.array_equal(I.cpu().numpy(), Io)
 
 
+@pytest.mark.parametrize("bad", [np.nan, np.inf])
+@pytest.mark.parametrize("where", ["cand", "query"])
+def test_knn_deferred_check(cuda, bad, where):
+    """mepol_knn_deferred: no host synchronisation inside the call; the rejection comes from
+    the returned check (same ValueError), and a clean call's result is bit-identical to the
+    synchronous entry point's."""
+    from mepol_amd import ops
+
+    X = np.random.default_rng(1).standard_normal((3000, 29)).astype(np.float32)
+    Q = X[:500].copy()
+    Xd, Qd = torch.as_tensor(X, device="cuda"), torch.as_tensor(Q, device="cuda")
+    D, I, _, chk = ops.knn(Xd, 31, query=Qd, defer_check=True)
+    chk.raise_if_invalid()
+    D2, I2, _ = ops.knn(Xd, 31, query=Qd)
+    assert torch.equal(D, D2) and torch.equal(I, I2)
+    (X if where == "cand" else Q)[77, 3] = bad
+    *_, chk = ops.knn(torch.as_tensor(X, device="cuda"), 31, query=torch.as_tensor(Q, device="cuda"),
+                      defer_check=True)
+    with pytest.raises(ValueError, match="NaN or infinity"):
+        chk.raise_if_invalid()
+
+
+def test_make_particle_batch_rejects_non_finite(cuda):
+    """The epoch's k-NN (deferred check) raises sklearn's ValueError before returning."""
+    from mepol_amd.algorithms import mepol as M
+
+    X = torch.randn(400, 2, device="cuda")
+    X[17, 1] = float("nan")
+    st = torch.zeros(4, 101, 2, dtype=torch.float64, device="cuda")
+    ac = torch.zeros(4, 100, 1, dtype=torch.float64, device="cuda")
+    rl = torch.full((4, 1), 100, dtype=torch.int64, device="cuda")
+    with pytest.raises(ValueError, match="NaN or infinity"):
+        M.make_particle_batch(st, ac, rl, X, 4)
+
+
 def test_knn_fallback_heavy_input_matches_oracle(cuda):
     """Many uncertified queries (heavy duplicate clusters with near-ties): the chunked
     exhaustive path (exact_kernel over the whole grid + exact_merge_kernel) answers them, and the

@@ -1,0 +1,19 @@
+#!/bin/bash
+# round 4: k-NN parity + timing, main library vs A/B variant libraries given as arguments
+set -o pipefail
+out=gpurun_out/${1:-r4k3}; shift
+mkdir -p $out
+timeout -k 10 400 python -u -m pytest tests/test_gpu_knn.py -x -q --timeout 120 --timeout-method thread > $out/knn_tests.log 2>&1 || { tail -30 $out/knn_tests.log; exit 1; }
+tail -2 $out/knn_tests.log
+for cfg in "" "--nq 25000" "--d 47" "--n 500000 --d 63 --kp1 51"; do
+  for lib in main "$@"; do
+    echo "== $cfg lib=$lib"
+    if [ $lib = main ]; then L=mepol_amd/libmepol_amd.so; else L=mepol_amd/libmepol_amd_$lib.so; fi
+    MEPOL_AMD_LIB=$L timeout -k 10 120 python -u tools/knn_probe.py $cfg --reps 4 2>&1 | tail -1 || exit 1
+  done
+done | tee $out/probe.log
+cd /tmp && export TMPDIR=/tmp && cd - >/dev/null
+timeout -k 10 200 rocprofv3 --kernel-trace -d $out/tr -o run -- python3 tools/knn_probe.py --nq 25000 --reps 2 > $out/tr.log 2>&1 || exit 1
+timeout -k 10 200 rocprofv3 --kernel-trace -d $out/tr3 -o run -- python3 tools/knn_probe.py --reps 2 > $out/tr3.log 2>&1 || exit 1
+python3 tools/kstats.py $out/tr/run_results.db 8
+python3 tools/kstats.py $out/tr3/run_results.db 8
