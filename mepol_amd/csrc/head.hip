@@ -512,9 +512,12 @@ static int reduce_records(const double* part, int nb, int64_t m, int AH, int A, 
   return 0;
 }
 
+#ifndef MEPOL_HEAD_BWD_MAXB
+#define MEPOL_HEAD_BWD_MAXB 512  // head_bwd_kernel blocks (partial records) at most
+#endif
 static int grid_bwd(int64_t N) {
   const int64_t waves = (N + 31) / 32;  // >= 32 rows per wave
-  return (int)std::max<int64_t>(1, std::min<int64_t>(512, (waves + 3) / 4));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(MEPOL_HEAD_BWD_MAXB, (waves + 3) / 4));
 }
 
 }  // namespace head
