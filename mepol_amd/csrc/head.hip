@@ -165,6 +165,14 @@ __global__ __launch_bounds__(256) void head_fwd16_kernel(
   }
 }
 
+// v from lane `lane` into an SGPR pair (wave-uniform).
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 // Per-block partial records [dW (A*H) | db (A) | dls (A)], reduced by reduce_partials_kernel.
 template <int AP, int NC>
 __global__ __launch_bounds__(256) void head_bwd_kernel(
@@ -184,20 +192,13 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     sW[e] = (c < H && a < A) ? Wm[a * H + c] : 0.0;
   }
   __syncthreads();
-  __shared__ double sInv[AP];
-  if (threadIdx.x < AP) {
-    const int a = threadIdx.x;
-    const double e = (a < A) ? exp(log_std[a]) : 1.0;
-    const double sd = e + kStdEps;
-    sInv[a] = 1.0 / (sd * sd);
-  }
-  double es3 = 0.0;  // lane a (< A) owns component a of db / dlog_std
+  double es3 = 0.0, inv = 0.0;  // lane a (< A) owns component a of dmu / db / dlog_std
   if (l < A) {
     const double e = exp(log_std[l]);
     const double sd = e + kStdEps;
     es3 = e / (sd * sd * sd);
+    inv = 1.0 / (sd * sd);
   }
-  __syncthreads();
   double accW[NC][AP];
 #pragma unroll
   for (int j = 0; j < NC; ++j)
@@ -210,18 +211,24 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
     bzr[j] = (bz && l + 64 * j < H) ? bz[l + 64 * j] : 0.0;
     accz[j] = 0.0;
   }
-  // kPF rows in flight per wave: z row (VGPRs) + its row-uniform g / act / mu (SGPRs) are
-  // loaded kPF rows ahead (register ring; slots are compile-time after unrolling).
+  // kPF rows in flight per wave: the z row, g (broadcast) and act / mu (lane a: component a)
+  // are loaded kPF rows ahead (register ring; slots are compile-time after unrolling).
   constexpr int kPF = MEPOL_HEAD_BWD_PF;
   struct Slot {
     double z[NC];
-    double g, av[AP], mv[AP];
+    double g, av, mv;
   };
   Slot ring[kPF];
   // Unconditional loads from clamped (in-bounds) addresses: no exec-mask branches around the
   // loads, so they issue back to back and stay in flight.  Values of clamped columns / rows /
   // components are never used (zero weights / bias, guarded stores, guarded rows, zeroed a >= A).
   const int64_t last = N - 1;
+  // Only vector loads (g through a laundered zero lane offset, so its address stays out of
+  // SGPRs): scalar loads of the prefetched row's g / act / mu shared lgkmcnt with the LDS reads
+  // of Wm, so the first LDS wait of a row also waited for the next row's scalars.
+  int vzero = 0;
+  asm volatile("" : "+v"(vzero));
+  const int la = l < A ? l : A - 1;
   auto load_slot = [&](Slot& dst, int64_t i) {
     const int64_t ic = i < N ? i : last;
     const double* zr = z + ic * H;
@@ -230,32 +237,24 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
       const int c = l + 64 * j;
       dst.z[j] = zr[c < H ? c : H - 1];
     }
-    dst.g = gl[ic];
-#pragma unroll
-    for (int a = 0; a < AP; ++a) {
-      const int ac = a < A ? a : A - 1;
-      dst.av[a] = act[ic * A + ac];
-      dst.mv[a] = mu[ic * A + ac];
-    }
+    dst.g = gl[ic + vzero];
+    dst.av = act[ic * A + la];
+    dst.mv = mu[ic * A + la];
   };
   auto row_step = [&](int64_t i, Slot& slot) {
     double zc[NC];
 #pragma unroll
     for (int j = 0; j < NC; ++j) zc[j] = slot.z[j];
     const double g = slot.g;
-    double dm[AP];  // every lane computes all dmu_a from row-uniform values
-    double db_l = 0.0, dls_l = 0.0;
+    // lane a < A forms dmu_a, then every lane takes dmu_0..A-1 into SGPRs (the same products in
+    // the same order as when every lane formed all of them)
+    const double d = (l < A) ? slot.av - slot.mv : 0.0;
+    const double dml = g * d * inv;
+    double dm[AP];
 #pragma unroll
-    for (int a = 0; a < AP; ++a) {
-      const double d = (a < A) ? slot.av[a] - slot.mv[a] : 0.0;
-      dm[a] = g * d * sInv[a];
-      if (a == l) {
-        db_l = dm[a];
-        dls_l = g * (-1.0 + d * d * es3);
-      }
-    }
-    accb += db_l;
-    accls += dls_l;
+    for (int a = 0; a < AP; ++a) dm[a] = readlane_d(dml, a);
+    accb += (l < A) ? dml : 0.0;
+    accls += (l < A) ? g * (-1.0 + d * d * es3) : 0.0;
     load_slot(slot, i + kPF * nwaves);
     double* dzr = dz ? dz + i * H : nullptr;
     int lo = l;
@@ -338,12 +337,6 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(
 // block walks rows in a fixed order (grid-stride), so each block's partial record
 // [dW (A*H) | db (A) | dls (A) | dbz (H)] is deterministic and reduce_partials_kernel sums the
 // records in a fixed order as for head_bwd_kernel.
-__device__ __forceinline__ double readlane_d(double v, int lane) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), lane);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
 
 template <int AP>
 __global__ __launch_bounds__(512) void head_bwd_wide_kernel(

@@ -1,8 +1,10 @@
 #!/bin/bash
-# round 4: head backward prefetch depth / grid A/B (tools/head_probe.py per library)
+# round 4: head backward parity + prefetch depth A/B (tools/head_probe.py per library)
 set -o pipefail
 out=gpurun_out/${1:-r4hp}; shift
 mkdir -p $out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_policy.py tests/test_gpu_device_loop.py -x -q --timeout 300 --timeout-method thread > $out/tests.log 2>&1 || { tail -30 $out/tests.log; exit 1; }
+tail -1 $out/tests.log
 for v in main "$@"; do
   L=mepol_amd/libmepol_amd.so; [ $v = main ] || L=mepol_amd/libmepol_amd_$v.so
   echo "== $v"
