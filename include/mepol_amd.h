@@ -33,8 +33,9 @@ extern "C" {
 #endif
 
 /* Bumped on every incompatible change of the signatures below (2: mepol_rollout_mlp takes a
- * workspace; mepol_gemm_dpp removed).  mepol_abi_version() returns the library's value. */
-#define MEPOL_ABI_VERSION 2
+ * workspace; mepol_gemm_dpp removed; 3: mepol_iw_normalize_gathered takes the per-rank
+ * trajectory sums).  mepol_abi_version() returns the library's value. */
+#define MEPOL_ABI_VERSION 3
 
 #define MEPOL_ERR_BAD_ARG 1001
 #define MEPOL_ERR_WORKSPACE 1002
@@ -116,11 +117,12 @@ int mepol_entropy_forward_emit(const double* w, const int32_t* idxT, const doubl
                                double eps, double* W_out, double* g_out, double* partials,
                                double* out4, double* vals, void* stream);
 /* Sharded off-policy iteration (mepol_amd/parallel.py), one launch each: the all-gathered
- * per-rank [u (n) | sum u] blocks normalised into w_glob [world n] (U summed in rank order), and
- * the replay's control scalars from the all-gathered raw sums (at offset off of each rank's block
- * of `stride` doubles): vals = {B - sums_cur[0], sum_kl / n_global}, then sums_cur = the sums. */
-int mepol_iw_normalize_gathered(const double* xu_all, int world, int64_t n, double* w_glob,
-                                void* stream);
+ * per-rank [u (n) | trajectory sums (nt)] blocks normalised into w_glob [world n] (U = the sum of
+ * all world * nt trajectory sums in one fixed order, the same on every rank), and the replay's
+ * control scalars from the all-gathered raw sums (at offset off of each rank's block of `stride`
+ * doubles): vals = {B - sums_cur[0], sum_kl / n_global}, then sums_cur = the sums. */
+int mepol_iw_normalize_gathered(const double* xu_all, int world, int64_t n, int nt,
+                                double* w_glob, void* stream);
 int mepol_sharded_emit(const double* x_all, int world, int64_t stride, int64_t off, double B,
                        int64_t n_global, double* sums_cur, double* vals, void* stream);
 

@@ -16,7 +16,7 @@ _c_dbl = ctypes.c_double
 _c_sz = ctypes.c_size_t
 _c_vp = ctypes.c_void_p
 
-ABI_VERSION = 2  # include/mepol_amd.h MEPOL_ABI_VERSION
+ABI_VERSION = 3  # include/mepol_amd.h MEPOL_ABI_VERSION
 
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 SIGNATURES = {
@@ -39,7 +39,7 @@ SIGNATURES = {
                               _c_dbl, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
     "mepol_entropy_forward_emit": [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_dbl, _c_dbl,
                               _c_dbl, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
-    "mepol_iw_normalize_gathered": [_c_vp, _c_int, _c_i64, _c_vp, _c_vp],
+    "mepol_iw_normalize_gathered": [_c_vp, _c_int, _c_i64, _c_int, _c_vp, _c_vp],
     "mepol_sharded_emit": [_c_vp, _c_int, _c_i64, _c_i64, _c_dbl, _c_i64, _c_vp, _c_vp, _c_vp],
     "mepol_csr_workspace_size": [_c_i64, _c_int, _c_i64, ctypes.POINTER(_c_sz)],
     "mepol_csr_build": [_c_vp, _c_i64, _c_int, _c_i64, _c_i64, _c_i64, _c_vp, _c_vp, _c_vp, _c_sz,

@@ -122,6 +122,7 @@ class DeviceIteration:
         self.fused_dh1 = (ops.dh1_layer1_ok(self.x.shape[1], W2.shape[0])
                           and os.environ.get("MEPOL_FUSED_DH1", "1") != "0")
         self.neg_one = torch.full((), -1.0, **f64)
+        self.W2t = torch.empty((W2.shape[1], W2.shape[0]), **f64) if self.fused_dh1 else None
         # every body takes its optimizer step through _optim_step, which leaves theta_t in the
         # replay's shadow (off_policy_optimization then copies it into last_valid only when it
         # needs it, not after every accepted step)
@@ -280,34 +281,46 @@ class DeviceIteration:
         ops.head_forward(self.z2, Wm, bm, ls, self.act, bz=b2, mu_out=self.mu,
                          logp_out=self.logp)
 
-    def _backward(self, grad):
+    def _backward(self, grad, outs=None):
         """(dW1, db1, dW2, db2, dWm, dbm, dls) from dH/dlogp: the _TwoLayerLogp backward.
+        `outs`: optional tensors of those seven shapes the kernels write into (the sharded
+        iteration passes views of its flat all-reduce buffer: no concatenation launch).
 
         Head backward, then dW2 (split-K GEMM, forked stream) concurrent with the fused
         dh1 -> layer-1 backward (measured: faster than dh1 first with dW2 overlapping the
         layer-1 backward, and than splitting dW2 across both phases)."""
         W1, b1, W2, b2, Wm, bm, ls = self.named
         cur = torch.cuda.current_stream()
-        # W2^T for the fused dh1 kernel, on this stream: on a forked one the small copy kernel
-        # would queue behind the dW2 GEMM's workgroups
-        W2t = W2.t().contiguous() if self.fused_dh1 else None
+        # W2^T for the fused dh1 kernel, on this stream (measured: as a branch on the fork
+        # stream under the forward it delayed the forward's start by ~12 us, more than the copy)
+        if self.fused_dh1:
+            self.W2t.copy_(W2.t())
+        W2t = self.W2t if self.fused_dh1 else None
         self.fork.wait_stream(cur)
         self.s_gemm.wait_stream(cur)
+        o = outs if outs is not None else (None,) * 7
+        head_outs = None if outs is None else (o[4], o[5], o[6], o[3])
         dz2, dWm, dbm, dls, db2 = ops.head_backward(grad, self.z2, Wm, ls, self.act, self.mu,
-                                                    bz=b2, need_dz=True, ws=self.ws_head)
+                                                    bz=b2, need_dz=True, ws=self.ws_head,
+                                                    outs=head_outs)
         e_h = torch.cuda.Event()
         e_h.record(cur)
         self.fork.wait_event(e_h)
         with torch.cuda.stream(self.fork):
-            dW2 = _weight_grad(dz2, self.h1)
+            dW2 = _weight_grad(dz2, self.h1, out=o[2])
         self.s_gemm.wait_event(e_h)
         with torch.cuda.stream(self.s_gemm):
             if self.fused_dh1:  # dh1 stays on chip (csrc/gemm.hip)
                 dh1 = None
-                dW1, db1 = ops.dh1_layer1_backward(dz2, W2t, self.h1, self.x, ws=self.ws_dh1)
+                dW1, db1 = ops.dh1_layer1_backward(dz2, W2t, self.h1, self.x, ws=self.ws_dh1,
+                                                   dW_out=o[0], db_out=o[1])
             else:
                 dh1 = torch.mm(dz2, W2)
                 dW1, db1 = ops.layer_backward(dh1, self.h1, self.x, ws=self.ws_layer)
+                if outs is not None:
+                    o[0].copy_(dW1)
+                    o[1].copy_(db1)
+                    dW1, db1 = o[0], o[1]
         cur.wait_stream(self.fork)
         cur.wait_stream(self.s_gemm)
         del dz2, dh1

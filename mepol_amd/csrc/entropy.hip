@@ -71,8 +71,19 @@ __global__ __launch_bounds__(256) void iw_scan_kernel(const double* __restrict__
 
 // Deterministic block-redundant reduction of a short array (every block gets the same value).
 __device__ double block_reduce_array(const double* __restrict__ a, int64_t n, double* sh) {
+  // each thread adds a[tid], a[tid + bd], ... in that order; 8 loads in flight per step (the
+  // sharded reverse scan sums every rank's gamma partials, ~12k values per block)
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += blockDim.x) s += a[i];
+  const int64_t bd = blockDim.x;
+  int64_t i = threadIdx.x;
+  for (; i + 7 * bd < n; i += 8 * bd) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = a[i + u * bd];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  for (; i < n; i += bd) s += a[i];
   s = wave_sum(s);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
   if (l == 0) sh[w] = s;
@@ -380,16 +391,32 @@ extern "C" int mepol_entropy_reverse_scan(const double* gamma, const double* w,
 }
 
 // ---- sharded iteration helpers (parallel.py ShardedIteration, one launch each) -------------
-// w_glob[r n + i] = xu_all[r (n + 1) + i] / U, U = sum_r xu_all[r (n + 1) + n] in rank order:
-// the all-gathered [u | sum u] blocks of every rank normalised in one pass (no copy, no sum).
-__global__ void iw_normalize_gathered_kernel(const double* __restrict__ xu_all, int world,
-                                             int64_t n, double* __restrict__ w_glob) {
-  double U = 0.0;
-  for (int r = 0; r < world; ++r) U += xu_all[(int64_t)r * (n + 1) + n];
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// w_glob[r n + i] = xu_all[r (n + nt) + i] / U, U = the sum of the world * nt trajectory sums
+// xu_all[r (n + nt) + n + t]: the all-gathered [u | trajectory sums] blocks of every rank
+// normalised in one pass.  Every block forms U with the same fixed tree (a strided partial per
+// thread, then pairwise in LDS), so every block of every rank holds the same bits.
+constexpr int kGatherThreads = 256;
+__global__ __launch_bounds__(kGatherThreads) void iw_normalize_gathered_kernel(
+    const double* __restrict__ xu_all, int world, int64_t n, int nt, double* __restrict__ w_glob) {
+  __shared__ double red[kGatherThreads];
+  const int tid = threadIdx.x;
+  const int64_t tot = (int64_t)world * nt;
+  double p = 0.0;
+  for (int64_t e = tid; e < tot; e += kGatherThreads) {
+    const int64_t r = e / nt, t = e % nt;
+    p += xu_all[r * (n + nt) + n + t];
+  }
+  red[tid] = p;
+  __syncthreads();
+  for (int s = kGatherThreads / 2; s > 0; s >>= 1) {
+    if (tid < s) red[tid] += red[tid + s];
+    __syncthreads();
+  }
+  const double U = red[0];
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + tid;
   if (e >= (int64_t)world * n) return;
   const int64_t r = e / n, i = e % n;
-  w_glob[e] = xu_all[r * (n + 1) + i] / U;
+  w_glob[e] = xu_all[r * (n + nt) + i] / U;
 }
 
 // The two control scalars of a sharded replay from the all-gathered raw sums (stride apart,
@@ -410,15 +437,16 @@ __global__ void sharded_emit_kernel(const double* __restrict__ x_all, int world,
   sums_cur[1] = s1;
 }
 
-extern "C" int mepol_iw_normalize_gathered(const double* xu_all, int world, int64_t n,
+extern "C" int mepol_iw_normalize_gathered(const double* xu_all, int world, int64_t n, int nt,
                                            double* w_glob, void* stream) {
-  if (world <= 0 || n <= 0 || !xu_all || !w_glob) {
+  if (world <= 0 || n <= 0 || nt <= 0 || !xu_all || !w_glob) {
     set_error("mepol_iw_normalize_gathered: bad arguments");
     return kErrBadArg;
   }
   const int64_t tot = (int64_t)world * n;
-  hipLaunchKernelGGL(iw_normalize_gathered_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256),
-                     0, (hipStream_t)stream, xu_all, world, n, w_glob);
+  hipLaunchKernelGGL(iw_normalize_gathered_kernel,
+                     dim3((unsigned)((tot + kGatherThreads - 1) / kGatherThreads)),
+                     dim3(kGatherThreads), 0, (hipStream_t)stream, xu_all, world, n, nt, w_glob);
   MEPOL_CHECK_LAUNCH();
   return 0;
 }

@@ -163,7 +163,8 @@ def knn_exact(cand, kp1, query=None, want_int64=True):
     return D, I, I32T
 
 
-def iw_forward(logp_t, logp_b, offsets, n_particles, normalize=True, w_out=None, u_out=None):
+def iw_forward(logp_t, logp_b, offsets, n_particles, normalize=True, w_out=None, u_out=None,
+               ts_out=None):
     """u = exp(segmented cumsum(logp_t - logp_b)); w = u / sum(u).
 
     logp_t/logp_b: f64 [nt, T_stride]; offsets: int64 [nt+1] particle offsets.
@@ -175,7 +176,7 @@ def iw_forward(logp_t, logp_b, offsets, n_particles, normalize=True, w_out=None,
     lt = logp_t.contiguous()
     lb = logp_b.contiguous()
     u = u_out if u_out is not None else torch.empty(n_particles, dtype=torch.float64, device=dev)
-    ts = torch.empty(nt, dtype=torch.float64, device=dev)
+    ts = ts_out if ts_out is not None else torch.empty(nt, dtype=torch.float64, device=dev)
     w = (w_out if w_out is not None else torch.empty(n_particles, dtype=torch.float64,
                                                      device=dev)) if normalize else None
     U = torch.empty((), dtype=torch.float64, device=dev) if normalize else None
@@ -219,10 +220,10 @@ def entropy_forward(w, idxT, D, k, ns, G, B, eps, n_w=None, g_out=None, out4=Non
     return out4, W, g
 
 
-def iw_normalize_gathered(xu_all, world, n, w_out):
-    """w_out [world n] <- the all-gathered [u | sum u] blocks (world x (n + 1)) normalised by
-    the rank-order sum of their totals."""
-    call("mepol_iw_normalize_gathered", ptr(xu_all), world, n, ptr(w_out), _stream())
+def iw_normalize_gathered(xu_all, world, n, nt, w_out):
+    """w_out [world n] <- the all-gathered [u | per-trajectory sums] blocks (world x (n + nt))
+    normalised by the fixed-order sum of all ranks' trajectory sums."""
+    call("mepol_iw_normalize_gathered", ptr(xu_all), world, n, nt, ptr(w_out), _stream())
     return w_out
 
 
@@ -251,12 +252,17 @@ def csr_build(idxT, k, n_own, col_offset=0, row_offset=0, nq=None):
     return off, rows
 
 
+def entropy_gamma_nparts(n_own):
+    """Block partials entropy_gamma returns: one per 256-thread block (16 lanes per particle),
+    at most 2048 blocks (csrc/entropy.hip)."""
+    return min((n_own * 16 + 255) // 256, 2048)
+
+
 def entropy_gamma(g, w_own, csr_off, csr_rows):
     n_own = w_own.numel()
     dev = w_own.device
     gamma = torch.empty(n_own, dtype=torch.float64, device=dev)
-    # one partial per 256-thread block (16 lanes per particle), at most 2048 blocks
-    nparts = min((n_own * 16 + 255) // 256, 2048)
+    nparts = entropy_gamma_nparts(n_own)
     partials = torch.empty(max(nparts, 1), dtype=torch.float64, device=dev)
     call("mepol_entropy_gamma", ptr(g), ptr(w_own), ptr(csr_off), ptr(csr_rows), n_own,
          ptr(gamma), ptr(partials), _stream())
@@ -282,9 +288,11 @@ def head_forward(z, Wm, bm, log_std, act, bz=None, mu_out=None, logp_out=None):
     return mu, logp
 
 
-def head_backward(grad_logp, z, Wm, log_std, act, mu, bz=None, need_dz=True, ws=None):
+def head_backward(grad_logp, z, Wm, log_std, act, mu, bz=None, need_dz=True, ws=None,
+                  outs=None):
     """Returns (dz or None, dWm, dbm, dlog_std, dbz or None).  `ws`: caller-owned scratch
-    (head_workspace); default: the per-stream eager cache."""
+    (head_workspace); default: the per-stream eager cache.  `outs`: optional (dWm, dbm,
+    dlog_std, dbz) tensors to write instead of fresh ones."""
     import ctypes
 
     n, h = z.shape
@@ -295,10 +303,14 @@ def head_backward(grad_logp, z, Wm, log_std, act, mu, bz=None, need_dz=True, ws=
         call("mepol_head_workspace_size", n, h, a, ctypes.byref(nbytes))
         ws = _workspace(dev, nbytes.value, tag="head")
     dz = torch.empty_like(z) if need_dz else None
-    dWm = torch.empty_like(Wm)
-    dbm = torch.empty(a, dtype=torch.float64, device=dev)
-    dls = torch.empty(a, dtype=torch.float64, device=dev)
-    dbz = torch.empty(h, dtype=torch.float64, device=dev) if bz is not None else None
+    if outs is not None:
+        dWm, dbm, dls, dbz = outs
+        assert all(t is None or t.is_contiguous() for t in outs)
+    else:
+        dWm = torch.empty_like(Wm)
+        dbm = torch.empty(a, dtype=torch.float64, device=dev)
+        dls = torch.empty(a, dtype=torch.float64, device=dev)
+        dbz = torch.empty(h, dtype=torch.float64, device=dev) if bz is not None else None
     call("mepol_head_backward", ptr(grad_logp), ptr(z), n, h, ptr(bz), ptr(Wm), ptr(log_std),
          ptr(act), ptr(mu), a, ptr(dz), ptr(dWm), ptr(dbm), ptr(dls), ptr(dbz), ptr(ws), ws.numel(),
          _stream())
@@ -342,7 +354,7 @@ def dh1_layer1_ok(in_features, hidden1):
     return in_features <= DH1_L1_MAX_IN and hidden1 % 2 == 0
 
 
-def dh1_layer1_backward(dz2, W2t, h1, x, ws=None):
+def dh1_layer1_backward(dz2, W2t, h1, x, ws=None, dW_out=None, db_out=None):
     """(dW1, db1) of h1 = relu(x W1^T + b1) from dz2 = dL/dz2 [n, h1w] and W2t = W2^T
     [h0, h1w]: dh1 = dz2 W2 is reduced on chip (csrc/gemm.hip), never written."""
     n, k = dz2.shape
@@ -355,8 +367,10 @@ def dh1_layer1_backward(dz2, W2t, h1, x, ws=None):
         nbytes = ctypes.c_size_t()
         call("mepol_dh1_layer1_workspace_size", n, h0, f, ctypes.byref(nbytes))
         ws = _workspace(x.device, nbytes.value, tag="dh1l1")
-    dW = torch.empty((h0, f), dtype=torch.float64, device=x.device)
-    db = torch.empty(h0, dtype=torch.float64, device=x.device)
+    dW = dW_out if dW_out is not None else torch.empty((h0, f), dtype=torch.float64,
+                                                      device=x.device)
+    db = db_out if db_out is not None else torch.empty(h0, dtype=torch.float64, device=x.device)
+    assert dW.is_contiguous() and db.is_contiguous()
     call("mepol_dh1_layer1_backward", ptr(dz2), n, k, ptr(W2t), h0, ptr(h1), ptr(x), f, ptr(dW),
          ptr(db), ptr(ws), ws.numel(), _stream())
     return dW, db

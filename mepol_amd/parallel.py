@@ -337,18 +337,19 @@ class ShardedIteration(DeviceIteration):
     H(theta_t+1) and dH/dW, kept in static buffers (``_prime`` fills them before the first replay
     and after a rejected step).  Collectives per replay (every rank issues the same sequence):
 
-      1. all-gather of one f64: the per-rank partial of S = sum_j gamma_j w_j   (8 B per rank)
+      1. all-gather of the gamma kernel's block partials of S = sum_j gamma_j w_j (<= 2048 f64)
       2. all-reduce of the flattened policy gradients                       (~1.1 MB at C3)
-      3. all-gather of [u (n_local), sum u]: unnormalised weights + normaliser (n_local + 1 f64)
+      3. all-gather of [u (n_local), trajectory sums]: weights + normaliser terms (n_local + nt)
       4. all-gather of [dH/dW (n_local), H, KL, H-sum, KL-sum]                 (n_local + 4 f64)
 
     Reductions over ranks are fixed-order sums of gathered values, so every rank holds the same
     bits and takes the same accept/backtrack branch (mepol.py:441-476).  The gathered blocks are
     read where they land: the weights are normalised straight out of the gather buffer
     (mepol_iw_normalize_gathered), the gamma kernel reads dH/dW there through CSR row ids
-    remapped once per epoch to that layout, the entropy pass writes its sums into the block it
-    sends, the gradients are concatenated into a persistent flat buffer that is all-reduced in
-    place, and one launch (mepol_sharded_emit) forms the control scalars."""
+    remapped once per epoch to that layout, the reverse scan sums the gathered S partials, the
+    entropy pass writes its sums into the block it sends, the backward kernels write the
+    gradients into views of a persistent flat buffer that is all-reduced in place, and one
+    launch (mepol_sharded_emit) forms the control scalars."""
 
     def __init__(self, tgt, optimizer, ep, G, B, ns, eps):
         super().__init__(tgt, optimizer, _LocalView(ep), ep.k, G, B, ns, eps)
@@ -358,23 +359,25 @@ class ShardedIteration(DeviceIteration):
         self.ep = ep
         f64 = dict(dtype=torch.float64, device=self.device)
         n, W = self.N, self.world
-        self.xs = torch.zeros(1, **f64)
-        self.xs_all = torch.zeros(W, **f64)
-        self.xu = torch.zeros(n + 1, **f64)
-        self.xu_all = torch.zeros(W * (n + 1), **f64)
+        self.nparts = self.ep.ops.entropy_gamma_nparts(n)
+        self.xs_all = torch.zeros(W * self.nparts, **f64)  # every rank's gamma block partials
+        self.xu = torch.zeros(n + self.nt, **f64)         # [u | trajectory sums]
+        self.xu_all = torch.zeros(W * (n + self.nt), **f64)
         self.xg = torch.zeros(n + 4, **f64)               # [dH/dW | H, KL, H-sum, KL-sum]
         self.xg_all = torch.zeros(W * (n + 4), **f64)     # dH/dW at theta_t of every particle
         self.w_glob = torch.zeros(self.N_global, **f64)   # importance weights at theta_t
         self.sums_cur = torch.zeros(2, **f64)             # [H-sum, KL-sum] at theta_t
         self.csr_rows_x = torch.empty_like(self.csr_rows)  # CSR ids in the xg_all layout
         # flat gradient buffer (all-reduced in place) and its per-parameter views, in the
-        # optimizer's parameter order
+        # optimizer's parameter order; the backward kernels write straight into the views
         sizes = [p.numel() for p in self.params]
         self.flat_grad = torch.zeros(sum(sizes), **f64)
         self.grad_views, o = [], 0
         for p, sz in zip(self.params, sizes):
             self.grad_views.append(self.flat_grad[o:o + sz].view_as(p))
             o += sz
+        view_of = {id(p): v for p, v in zip(self.params, self.grad_views)}
+        self.grad_outs = tuple(view_of[id(p)] for p in self.named)
 
     def matches_epoch(self, tgt, optimizer, ep, G, B, ns, eps):
         return (self.matches(tgt, optimizer, _LocalView(ep), ep.k, G, B, ns, eps)
@@ -400,11 +403,10 @@ class ShardedIteration(DeviceIteration):
         ranks: collectives 3 and 4.  w_glob and xg_all are overwritten."""
         ops, n, W = self.ep.ops, self.N, self.world
         lt = self.logp.view(self.nt, self.T)
-        _, ts, _, _ = ops.iw_forward(lt, self.logp_b, self.offsets, n, normalize=False,
-                                     u_out=self.xu[:n])
-        torch.sum(ts, 0, keepdim=True, out=self.xu[n:])
+        ops.iw_forward(lt, self.logp_b, self.offsets, n, normalize=False, u_out=self.xu[:n],
+                       ts_out=self.xu[n:])
         self._gather_into(self.xu_all, self.xu)
-        ops.iw_normalize_gathered(self.xu_all, W, n, self.w_glob)
+        ops.iw_normalize_gathered(self.xu_all, W, n, self.nt, self.w_glob)
         ops.entropy_forward(self.w_glob, self.idx32T, self.D, self.k, self.ns, self.G, self.B,
                             self.eps, n_w=self.N_global, g_out=self.xg[:n], out4=self.xg[n:])
         self._gather_into(self.xg_all, self.xg)
@@ -426,14 +428,13 @@ class ShardedIteration(DeviceIteration):
         w_local = self.w_glob[self.R0:self.R0 + n]
         gamma, partials, nparts = ops.entropy_gamma(self.xg_all, w_local, self.csr_off,
                                                     self.csr_rows_x)
-        torch.sum(partials[:nparts], 0, keepdim=True, out=self.xs)
-        self._gather_into(self.xs_all, self.xs)
-        S = self.xs_all.sum()
-        grad = ops.entropy_reverse_scan(gamma, w_local, partials, nparts, self.offsets, nt, T,
-                                        self.neg_one, S_ext=S)
-        got = self._backward(grad.view(-1))
-        grad_of = {id(p): t for p, t in zip(self.named, got)}
-        torch.cat([grad_of[id(p)].reshape(-1) for p in self.params], out=self.flat_grad)
+        assert nparts == self.nparts
+        # every rank's block partials of S = sum_j gamma_j w_j; the reverse scan sums all of
+        # them in one fixed order (the same bits on every rank)
+        self._gather_into(self.xs_all, partials[:nparts])
+        grad = ops.entropy_reverse_scan(gamma, w_local, self.xs_all, self.world * nparts,
+                                        self.offsets, nt, T, self.neg_one)
+        self._backward(grad.view(-1), outs=self.grad_outs)
         self.dist.all_reduce(self.flat_grad, group=self.group)  # ShardedEpoch.allreduce_grads
         self._optim_step(self.grad_views)
         # KL at theta_t+1 (ShardedEpoch.compute_kl); H(theta_t+1) and dH/dW for the next replay
