@@ -57,24 +57,21 @@ __device__ __forceinline__ float list_at(const float (&ld)[LIST], int j) {
 
 template <int LIST>
 __device__ __forceinline__ void flush_buffer(float (&ld)[LIST], int (&li)[LIST], float& thr, int& cnt,
-                                             const float (*bv)[64], const int (*bi)[64], int l,
-                                             float thr0, int keep = 0) {
+                                             const float2 (*buf)[64], int l, float thr0,
+                                             int keep = 0) {
   const int mc = wave_max_i(cnt);
   // entry e + 1 is read from LDS while entry e is inserted (the read latency would otherwise
   // sit in front of every insertion)
-  float x = bv[0][l];
-  int xi = bi[0][l];
+  float2 cur = buf[0][l];
 #pragma nounroll
   for (int e = 0; e < mc; ++e) {
     const int en = min(e + 1, kBufCap - 1);
-    const float xn = bv[en][l];
-    const int xin = bi[en][l];
-    if (e < cnt && x < thr) {
-      list_insert<LIST>(ld, li, x, xi);
+    const float2 nxt = buf[en][l];
+    if (e < cnt && cur.x < thr) {
+      list_insert<LIST>(ld, li, cur.x, __float_as_int(cur.y));
       thr = ld[LIST - 1];
     }
-    x = xn;
-    xi = xin;
+    cur = nxt;
   }
   cnt = 0;
   // lanes l and l^32 serve the same query: the tighter of their maxima is a valid prune bound

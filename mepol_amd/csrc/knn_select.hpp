@@ -27,8 +27,8 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
                                                        float* __restrict__ out_v,
                                                        int* __restrict__ out_i,
                                                        int* __restrict__ seed) {
-  __shared__ float sbuf_v[4][kBufCap][64];
-  __shared__ int sbuf_i[4][kBufCap][64];
+  // per-lane insertion buffer: (value, index bits) pairs, one 8-byte LDS access per entry
+  __shared__ float2 sbuf[4][kBufCap][64];
   const int w = threadIdx.x >> 6;
   const int l = threadIdx.x & 63;
   // XCD-aware block mapping: workgroups go round-robin over the 8 XCDs by linear id, so with
@@ -160,8 +160,7 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
             for (int i = 0; i < 4; ++i) {
               const int r = 4 * g + i;
               if (acc[r] < thr) {
-                sbuf_v[w][cnt][l] = acc[r];
-                sbuf_i[w][cnt][l] = base + acc_row(r, l);
+                sbuf[w][cnt][l] = make_float2(acc[r], __int_as_float(base + acc_row(r, l)));
                 ++cnt;
               }
             }
@@ -171,14 +170,13 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           if (acc[r] < thr) {
-            sbuf_v[w][cnt][l] = acc[r];
-            sbuf_i[w][cnt][l] = base + acc_row(r, l);
+            sbuf[w][cnt][l] = make_float2(acc[r], __int_as_float(base + acc_row(r, l)));
             ++cnt;
           }
         }
       }
       if (__ballot(cnt > kBufCap - 16))
-        flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0, keep);
+        flush_buffer<LIST>(ld, li, thr, cnt, sbuf[w], l, thr0, keep);
     }
   };
   if constexpr (NB == 2) {
@@ -259,7 +257,7 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
       for (int v = 0; v < NV; ++v) asm volatile("" : "+v"(Bf[b][v]));
     process(accP, t - 1);
   }
-  flush_buffer<LIST>(ld, li, thr, cnt, sbuf_v[w], sbuf_i[w], l, thr0, keep);
+  flush_buffer<LIST>(ld, li, thr, cnt, sbuf[w], l, thr0, keep);
   // publish this range's final bound (the same in both lanes of the query)
   if (seed && qvalid && h == 0)
     __hip_atomic_fetch_min(seed + q, float_order_key(thr), __ATOMIC_RELAXED,
