@@ -149,7 +149,23 @@ __global__ __launch_bounds__(256, OCC) void select16_kernel(const _Float16* __re
     const float m = fminf(fminf(gm[0], gm[1]), fminf(gm[2], gm[3]));
     if (__ballot(m < thr)) {
       const int base = (int)(t * 32);
-      if constexpr (GATE == 4) {
+      if constexpr (GATE == 5) {
+        // row groups gated as below, the rows of a hit group branch-free: every lane of the
+        // group writes its value at its cursor and advances the cursor only when the value is
+        // under its bound (a later write overwrites a rejected one).  The cursor enters a tile
+        // at <= kBufCap - 16 (flush condition below), so the write index stays < kBufCap.
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          if (gm[g] < thr) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int r = 4 * g + i;
+              sbuf[w][cnt][l] = make_float2(acc[r], __int_as_float(base + acc_row(r, l)));
+              cnt += acc[r] < thr ? 1 : 0;
+            }
+          }
+        }
+      } else if constexpr (GATE == 4) {
         // hierarchical gating: a row group is skipped by the whole wave unless some lane has a
         // value under its bound there (4 group tests + 4 row tests per hit group instead of 16
         // row tests per hit tile)
@@ -317,11 +333,12 @@ static void launch_select16_gate(const SelectArgs& a, hipStream_t st) {
 #undef MEPOL_SEL16O
 }
 
-// MEPOL_KNN_GATE=1: round 3's per-row gating of a hit tile (A/B probe); default 4 (row groups).
+// MEPOL_KNN_GATE (A/B probe): 1 = round 3's per-row gating of a hit tile, 4 = row groups with
+// a branch per row, 5 (default) = row groups with branch-free rows.
 static int select_gate() {
   static const int v = [] {
     const char* e = getenv("MEPOL_KNN_GATE");
-    return (e && e[0] == '1') ? 1 : 4;
+    return (e && e[0] == '1') ? 1 : (e && e[0] == '4') ? 4 : 5;
   }();
   return v;
 }
@@ -329,6 +346,10 @@ static int select_gate() {
 template <int KS16, int NH>
 static void launch_select16_ks(const SelectArgs& a, hipStream_t st) {
   if constexpr (NH == 1) {
+    if (select_gate() == 5) {
+      launch_select16_gate<KS16, NH, 5>(a, st);
+      return;
+    }
     if (select_gate() == 4) {
       launch_select16_gate<KS16, NH, 4>(a, st);
       return;
