@@ -281,10 +281,13 @@ class DeviceIteration:
         ops.head_forward(self.z2, Wm, bm, ls, self.act, bz=b2, mu_out=self.mu,
                          logp_out=self.logp)
 
-    def _backward(self, grad, outs=None):
+    def _backward(self, grad, outs=None, after_dW2=None):
         """(dW1, db1, dW2, db2, dWm, dbm, dls) from dH/dlogp: the _TwoLayerLogp backward.
         `outs`: optional tensors of those seven shapes the kernels write into (the sharded
         iteration passes views of its flat all-reduce buffer: no concatenation launch).
+        `after_dW2`: optional callable issued on the dW2 stream once dW2 and the head gradients
+        are written, concurrent with the dh1 / layer-1 backward (the sharded iteration starts
+        that bucket's all-reduce there).
 
         Head backward, then dW2 (split-K GEMM, forked stream) concurrent with the fused
         dh1 -> layer-1 backward (measured: faster than dh1 first with dW2 overlapping the
@@ -308,6 +311,8 @@ class DeviceIteration:
         self.fork.wait_event(e_h)
         with torch.cuda.stream(self.fork):
             dW2 = _weight_grad(dz2, self.h1, out=o[2])
+            if after_dW2 is not None:
+                after_dW2()
         self.s_gemm.wait_event(e_h)
         with torch.cuda.stream(self.s_gemm):
             if self.fused_dh1:  # dh1 stays on chip (csrc/gemm.hip)

@@ -338,7 +338,8 @@ class ShardedIteration(DeviceIteration):
     and after a rejected step).  Collectives per replay (every rank issues the same sequence):
 
       1. all-gather of the gamma kernel's block partials of S = sum_j gamma_j w_j (<= 2048 f64)
-      2. all-reduce of the flattened policy gradients                       (~1.1 MB at C3)
+      2. all-reduce of the flattened policy gradients, in two buckets: W2 / head (~0.97 MB at
+         C3, issued on the dW2 stream under the dh1 backward) and W1 / b1 (~0.1 MB)
       3. all-gather of [u (n_local), trajectory sums]: weights + normaliser terms (n_local + nt)
       4. all-gather of [dH/dW (n_local), H, KL, H-sum, KL-sum]                 (n_local + 4 f64)
 
@@ -378,6 +379,20 @@ class ShardedIteration(DeviceIteration):
             o += sz
         view_of = {id(p): v for p, v in zip(self.params, self.grad_views)}
         self.grad_outs = tuple(view_of[id(p)] for p in self.named)
+        # Two all-reduce buckets when the flat layout allows: [W2, b2, Wm, bm, log_std] (ready
+        # when the dW2 GEMM ends) reduced on the dW2 stream while the dh1 / layer-1 backward
+        # still runs, then [W1, b1].  Needs those five as one contiguous tail of flat_grad.
+        self.tail_off = None
+        offs = {id(p): v.data_ptr() for p, v in zip(self.params, self.grad_views)}
+        base = self.flat_grad.data_ptr()
+        first_tail = min(offs[id(p)] for p in self.named[2:]) - base
+        head_end = max(offs[id(p)] + p.numel() * 8 for p in self.named[:2]) - base
+        if head_end <= first_tail and first_tail % 8 == 0:
+            t0 = first_tail // 8
+            tail_elems = sum(p.numel() for p in self.named[2:])
+            if t0 + tail_elems == self.flat_grad.numel() and t0 == sum(p.numel()
+                                                                      for p in self.named[:2]):
+                self.tail_off = t0
 
     def matches_epoch(self, tgt, optimizer, ep, G, B, ns, eps):
         return (self.matches(tgt, optimizer, _LocalView(ep), ep.k, G, B, ns, eps)
@@ -434,8 +449,15 @@ class ShardedIteration(DeviceIteration):
         self._gather_into(self.xs_all, partials[:nparts])
         grad = ops.entropy_reverse_scan(gamma, w_local, self.xs_all, self.world * nparts,
                                         self.offsets, nt, T, self.neg_one)
-        self._backward(grad.view(-1), outs=self.grad_outs)
-        self.dist.all_reduce(self.flat_grad, group=self.group)  # ShardedEpoch.allreduce_grads
+        # ShardedEpoch.allreduce_grads: in two buckets when the layout allows (see __init__)
+        if self.tail_off is not None:
+            tail = self.flat_grad[self.tail_off:]
+            self._backward(grad.view(-1), outs=self.grad_outs,
+                           after_dW2=lambda: self.dist.all_reduce(tail, group=self.group))
+            self.dist.all_reduce(self.flat_grad[:self.tail_off], group=self.group)
+        else:
+            self._backward(grad.view(-1), outs=self.grad_outs)
+            self.dist.all_reduce(self.flat_grad, group=self.group)
         self._optim_step(self.grad_views)
         # KL at theta_t+1 (ShardedEpoch.compute_kl); H(theta_t+1) and dH/dW for the next replay
         self.forward()
