@@ -710,7 +710,7 @@ struct Plan {
   size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_part, off_cpad, off_seed, total;
 };
 
-static const int kListChoices[] = {8, 16, 24, 32, 40};
+static const int kListChoices[] = {8, 16, 22, 24, 32, 40};  // 22 = keep + 4 at k + 1 = 31
 
 static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Plan* P) {
   if (nc <= 0 || nq < 0 || d <= 0 || kp1 <= 0) {
@@ -740,8 +740,12 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   // than LIST16 of the query's nearest candidates only costs certification (exact path).
   P->keep = (kp1 + 1) / 2 + 2;
   P->LIST16 = 40;
+  static const bool no22 = [] {  // MEPOL_KNN_LIST22=0: skip the 22-entry lists (A/B probe)
+    const char* e = getenv("MEPOL_KNN_LIST22");
+    return e && e[0] == '0';
+  }();
   for (int v : kListChoices)
-    if (v >= P->keep + 4) {
+    if (v >= P->keep + 4 && !(no22 && v == 22)) {
       P->LIST16 = v;
       break;
     }

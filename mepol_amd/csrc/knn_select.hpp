@@ -315,6 +315,15 @@ static void launch_select16_gate(const SelectArgs& a, hipStream_t st) {
   switch (a.LIST16) {  // >= keep + 4 >= 7; split-candidate plans keep the instances that fit
     case 8: MEPOL_SEL16(8); break;
     case 16: MEPOL_SEL16(16); break;
+    case 22:
+      if constexpr (NH == 1 && KS16 <= 2) {
+        if (select_occ3()) {
+          MEPOL_SEL16O(22, 3);
+          break;
+        }
+      }
+      MEPOL_SEL16(22);
+      break;
     case 24:
       if constexpr (NH == 1 && KS16 <= 2) {
         if (select_occ3()) {
