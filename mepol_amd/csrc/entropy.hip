@@ -220,7 +220,19 @@ __global__ __launch_bounds__(256) void gamma_kernel(const double* __restrict__ g
        j += stride) {
     double gj = 0.0;
     const int32_t b = off[j], e = off[j + 1];
-    for (int32_t x = b + sub; x < e; x += kGammaLanes) gj += g[rows[x]];
+    // 4 of the lane's ids, then their 4 gathers, in flight together (clamped reads of the
+    // segment's last id past its end); the sum keeps the lane's order x = b + sub, +16, ...
+    for (int32_t x0 = b + sub; x0 < e; x0 += 4 * kGammaLanes) {
+      int32_t r[4];
+      double v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) r[u] = rows[min(x0 + u * kGammaLanes, e - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = g[r[u]];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (x0 + u * kGammaLanes < e) gj += v[u];
+    }
 #pragma unroll
     for (int m = kGammaLanes / 2; m >= 1; m >>= 1) gj += __shfl_xor(gj, m, kWave);
     if (sub == 0) {
