@@ -18,6 +18,7 @@ Differences a caller can observe (all documented in DESIGN.md):
   * rollout noise comes from torch's device generator, so trajectories are not the CPU
     reference's random stream (dynamics are; see tests/test_gpu_envs.py).
 """
+import atexit
 import math
 import os
 import time
@@ -96,6 +97,29 @@ class _RolloutGraph:
 
 
 _ROLLOUT_GRAPHS = weakref.WeakKeyDictionary()  # policy -> {key: _RolloutGraph}
+
+
+@atexit.register
+def _release_graphs_at_exit():
+    """Drop every captured graph (rollout, off-policy loop, sharded loop) while the HIP runtime
+    is still up: left to interpreter teardown they can be destroyed after it (a segfault at exit
+    was seen under rocprofv3)."""
+    try:
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+    except Exception:  # noqa: BLE001 - best effort at exit
+        pass
+    _ROLLOUT_GRAPHS.clear()
+    import sys
+
+    dl = sys.modules.get("mepol_amd.algorithms.device_loop")
+    if dl is not None:
+        for it in list(dl._CACHE.values()):
+            it.release()
+        dl._CACHE.clear()
+    par = sys.modules.get("mepol_amd.parallel")
+    if par is not None:
+        par.release_graphs()
 
 
 def _rollout_graph(policy, env_id, init, T, a_dim, nf):
@@ -290,13 +314,17 @@ def collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len
                                         "that can be equally split among workers"
     s32, a32, rtl32, ns32 = collect_particles_device(env, behavioral_policy, num_traj, traj_len,
                                                      state_filter)
+    # host copy of the lengths before the k-NN is queued: read after it, it would make the host
+    # wait for the whole k-NN and leave the GPU idle while the batch is set up
+    lens_host = rtl32.reshape(-1).to(torch.int64).cpu()
     # the k-NN's input check is read once the work behind it is queued (mepol_knn_deferred)
     D, I, I32T, check = ops.knn(ns32, k + 1, defer_check=True)
     states = s32.to(float_type)
     actions = a32.to(float_type)
     next_states = ns32.to(float_type)
     real_traj_lengths = rtl32.to(int_type)
-    batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T)
+    batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T,
+                            lengths=lens_host)
     P.register(I, batch)
     batch.csr(k)  # queued now: the GPU builds it while the host sets up the off-policy loop
     check.raise_if_invalid()  # sklearn's check_array ValueError, as kneighbors raises it
@@ -306,8 +334,10 @@ def collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len
 def make_particle_batch(states, actions, real_traj_lengths, next_states_f32, k):
     """Register a batch built from externally produced particles (e.g. a MuJoCo rollout or a
     synthetic benchmark batch): runs the GPU k-NN and returns the reference's 6-tuple."""
+    lens_host = real_traj_lengths.reshape(-1).to(torch.int64).cpu()  # before the k-NN: see above
     D, I, I32T, check = ops.knn(next_states_f32, k + 1, defer_check=True)
-    batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T)
+    batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T,
+                            lengths=lens_host)
     P.register(I, batch)
     batch.csr(k)  # queued now: the GPU builds it while the host sets up the off-policy loop
     check.raise_if_invalid()

@@ -25,19 +25,29 @@ def _param_key(policy):
 
 class ParticleBatch:
     def __init__(self, states, actions, real_traj_lengths, distances, indices, idx32T=None,
-                 device=None):
+                 device=None, lengths=None):
         dev = device if device is not None else (
             distances.device if distances.is_cuda else torch.device("cuda"))
         self.device = dev
         self.states = states.to(dev, torch.float64)
         self.actions = actions.to(dev, torch.float64)
         self.num_traj, self.T = self.actions.shape[0], self.actions.shape[1]
-        lens = real_traj_lengths.reshape(-1).to(torch.int64).cpu()
+        # `lengths`: the same values already on the host (the epoch path reads them before it
+        # queues the k-NN, so this constructor does not wait for the k-NN to finish)
+        lens = (lengths if lengths is not None
+                else real_traj_lengths.reshape(-1).to(torch.int64).cpu())
         self.lengths = lens
         self.dense = bool((lens == self.T).all())
         off = torch.zeros(self.num_traj + 1, dtype=torch.int64)
         off[1:] = torch.cumsum(lens, 0)
-        self.offsets = off.to(dev)
+        if lengths is not None and real_traj_lengths.is_cuda and real_traj_lengths.device == dev:
+            # the same offsets formed on the device: a copy of the host tensor would be a
+            # blocking transfer that waits for the k-NN queued before it
+            doff = torch.zeros(self.num_traj + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(real_traj_lengths.reshape(-1).to(torch.int64), 0, out=doff[1:])
+            self.offsets = doff
+        else:
+            self.offsets = off.to(dev)
         self.N = int(off[-1])
         nf = self.states.shape[-1]
         self.states_flat = self.states[:, : self.T].reshape(self.num_traj * self.T, nf).contiguous()

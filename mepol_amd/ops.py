@@ -5,6 +5,7 @@ must live on a ROCm device; dtypes follow the reference (f64 values, int64 indic
 API boundary; int32 indices internally).
 """
 import math
+import os
 
 import torch
 
@@ -80,13 +81,25 @@ def knn_plan(n_cand, n_query, d, kp1, split=0):
     return {"KS16": ks.value // 10, "nh": ks.value % 10, "LIST16": lst.value, "split": sp.value}
 
 
+class _NoCheck:
+    def raise_if_invalid(self):
+        pass
+
+
 class KnnInputCheck:
     """The input validation of a deferred k-NN call (mepol_knn_deferred): the two counts stay
     on the device, copied to pinned host memory in stream order; raise_if_invalid() waits for
     that copy only and raises what mepol_knn would have raised."""
 
+    _pinned = []  # reused pinned slots (a pinned allocation per call cost ~1 ms of host time)
+    _next = 0
+
     def __init__(self, invalid_dev):
-        self._host = torch.empty(2, dtype=torch.int32, pin_memory=True)
+        cls = KnnInputCheck
+        if not cls._pinned:
+            cls._pinned = [torch.empty(2, dtype=torch.int32, pin_memory=True) for _ in range(8)]
+        self._host = cls._pinned[cls._next]
+        cls._next = (cls._next + 1) % len(cls._pinned)
         memcpy_async(self._host, invalid_dev)
         self._event = torch.cuda.Event()
         self._event.record(torch.cuda.current_stream(invalid_dev.device))
@@ -134,6 +147,10 @@ def knn(cand, kp1, query=None, split=0, want_int64=True, return_fallback=False, 
     I32T = torch.empty((kp1, nq), dtype=torch.int32, device=dev)
     nfb = torch.zeros(1, dtype=torch.int32, device=dev)
     out = (D, I, I32T) + ((nfb,) if return_fallback else ())
+    if defer_check and os.environ.get("MEPOL_KNN_SYNC_CHECK") == "1":  # A/B probe
+        call("mepol_knn", ptr(cand), nc, ptr(query), nq, d, kp1, split, ptr(D), ptr(I), ptr(I32T),
+             ptr(nfb), ptr(ws), ws.numel(), _stream())
+        return out + (_NoCheck(),)
     if defer_check:
         invalid = torch.empty(2, dtype=torch.int32, device=dev)
         call("mepol_knn_deferred", ptr(cand), nc, ptr(query), nq, d, kp1, split, ptr(D), ptr(I),
