@@ -331,11 +331,17 @@ def collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len
     return states, actions, real_traj_lengths, next_states, D, I
 
 
-def make_particle_batch(states, actions, real_traj_lengths, next_states_f32, k):
+def make_particle_batch(states, actions, real_traj_lengths, next_states_f32, k,
+                        knn_events=None):
     """Register a batch built from externally produced particles (e.g. a MuJoCo rollout or a
-    synthetic benchmark batch): runs the GPU k-NN and returns the reference's 6-tuple."""
+    synthetic benchmark batch): runs the GPU k-NN and returns the reference's 6-tuple.
+    knn_events: optional (start, end) CUDA events recorded around the k-NN call alone."""
     lens_host = real_traj_lengths.reshape(-1).to(torch.int64).cpu()  # before the k-NN: see above
+    if knn_events is not None:
+        knn_events[0].record()
     D, I, I32T, check = ops.knn(next_states_f32, k + 1, defer_check=True)
+    if knn_events is not None:
+        knn_events[1].record()
     batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T,
                             lengths=lens_host)
     P.register(I, batch)
