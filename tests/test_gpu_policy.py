@@ -1,6 +1,9 @@
 """Fused HIP Gaussian head (csrc/head.hip) == the PyTorch GaussianPolicy.get_log_p math."""
+import numpy as np
 import pytest
 import torch
+
+from oracle import mepol_oracle as O
 
 pytestmark = pytest.mark.gpu
 
@@ -107,3 +110,28 @@ def test_policy_forward_kernel_matches_torch(cuda, n, nf, hidden, a):
     torch.testing.assert_close(z2, z2_ref, rtol=1e-12, atol=1e-12)
     torch.testing.assert_close(mu, mu_ref, rtol=1e-12, atol=1e-12)
     torch.testing.assert_close(logp, lp_ref, rtol=1e-12, atol=1e-11)
+
+
+@pytest.mark.parametrize("nf,hidden,a", [(29, [400, 300], 8), (47, [400, 300], 17),
+                                         (63, [400, 300], 20), (2, [300, 300], 2)])
+def test_fused_logp_and_mean_vs_oracle(cuda, nf, hidden, a):
+    """A2/A3 parity on the GPU against the oracle (not the build against itself): get_log_p and
+    the mean of the fused large-batch path (policy.py:21-51) vs oracle.log_p / mlp_mean, the
+    numpy restatement pinned on the reference's policy fixtures (tests/test_oracle_golden.py)."""
+    from mepol_amd import policy as P
+
+    torch.manual_seed(11)
+    pol = P.GaussianPolicy(hidden, nf, a, -0.6).cuda()
+    n = 20000
+    rng = np.random.default_rng(4)
+    s = torch.as_tensor(rng.standard_normal((n, nf)), device="cuda")
+    act = torch.as_tensor(0.5 * rng.standard_normal((n, a)), device="cuda")
+    assert pol._fused_head_ok(s, act)
+    sd = {k: v.detach().cpu().numpy() for k, v in pol.state_dict().items()}
+    with torch.no_grad():
+        lp = pol.get_log_p(s, act).cpu().numpy()
+        mu, _ = pol(s, deterministic=True)
+    ref_lp = O.log_p(sd, s.cpu().numpy(), act.cpu().numpy())
+    ref_mu = O.mlp_mean(sd, s.cpu().numpy())
+    np.testing.assert_allclose(lp, ref_lp, rtol=1e-11, atol=1e-11)
+    np.testing.assert_allclose(mu.cpu().numpy(), ref_mu, rtol=1e-11, atol=1e-12)
