@@ -401,14 +401,14 @@ def run(args):
     nq = N // shards
     F = 3.0 * d * nq * N                      # algorithmic flops
     knn_tflops = F / (knn_ms * 1e-3) / 1e12
-    # The selection (csrc/knn.hip, make_plan): f16 MFMA with the candidates' hi half (nh = 1,
-    # 2 products: q_hi, q_lo) or hi + lo halves (nh = 2, 3 products), 2 x K flops each per
-    # (query, candidate), K = 16*ceil((d+1)/16), f32 accumulate; then the certified f64 refine.
+    # The selection (csrc/knn.hip, make_plan): f16 MFMA with the candidates' hi half (nh = 1:
+    # 1 product per k-step at <= 3 k-steps, q_lo added at 4) or hi + lo halves (nh = 2, 3
+    # products), 2 x K flops each per (query, candidate) tile pair, K = 16*ceil((d+1)/16), f32
+    # accumulate; then the certified f64 refine.
     from mepol_amd import ops as _ops
 
     plan = _ops.knn_plan(N, nq, d, k + 1)
-    K16 = 16 * plan["KS16"]
-    knn_issued = (1 + plan["nh"]) * 2 * K16 * float(nq) * N
+    knn_issued = _ops.knn_issued_mfma_flops(N, nq, plan)
     knn_peak = PEAK_F16_TFLOPS
     knn_desc = (("f16 MFMA selection (candidate hi half x split query" if plan["nh"] == 1 else
                  "f16 MFMA selection (split candidate x split query, 3 products")
@@ -455,6 +455,8 @@ def run(args):
         "roofline": {"bound": "mfma", "achieved": round(knn_tflops, 2), "peak": knn_peak,
                      "unit": "TFLOP/s", "frac": round(knn_tflops / knn_peak, 4),
                      "mfma_issued_tflops": round(knn_issued / (knn_ms * 1e-3) / 1e12, 2),
+                     "mfma_issued_frac": round(knn_issued / (knn_ms * 1e-3) / 1e12 / knn_peak, 4),
+                     "mfma_products_per_kstep": plan["mfma_products"],
                      "traffic": traffic,
                      "kernel": ("k-NN call (norms + pack + select + refine + exact), HIP events "
                                 "around the call on its launch stream" if not sharded else

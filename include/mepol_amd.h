@@ -56,30 +56,39 @@ int mepol_memcpy_async(void* dst, const void* src, size_t bytes, void* stream);
  * arithmetic), rows ascending, ties by smaller index; idx_out [n_query, kp1] int64 (nullable);
  * idx32_out [kp1, n_query] int32 TRANSPOSED (nullable; the layout the entropy kernels read).
  * n_fallback_out (nullable, device int32): number of queries answered by the exhaustive path.
- * split_hint: 0 = automatic candidate split.  Fast path: d <= 63, kp1 <= 60.
+ * split_hint: 0 = automatic candidate split.  Any d >= 1 and any 1 <= kp1 <= n_cand (sklearn
+ * raises for kp1 > n_samples; so does this, MEPOL_ERR_BAD_ARG); n_cand < 2^31 - 64.  Plans:
+ * d <= 63 and kp1 <= 60 run the f16 MFMA screen + certified f64 re-rank (queries it cannot
+ * certify take the exhaustive scan); every other shape, and any input with a row whose f32
+ * squared norm overflows (the screen cannot scale it), is answered by the exhaustive f64 scan
+ * for every query (mepol_knn_plan_info reports *ks = 0 for such a plan).
  * Input validation (sklearn's check_array in fit/kneighbors): a NaN / inf coordinate in cand or
- * query returns MEPOL_ERR_BAD_ARG ("Input contains NaN or infinity"); a row whose f32 squared
- * norm overflows returns MEPOL_ERR_UNSUPPORTED.  The check synchronises `stream` once per call
- * (before the scan is launched), as the reference's kneighbors call blocks. */
+ * query returns MEPOL_ERR_BAD_ARG ("Input contains NaN or infinity").  The check synchronises
+ * `stream` once per call (before the scan is launched), as the reference's kneighbors call
+ * blocks. */
 int mepol_knn_workspace_size(int64_t n_cand, int64_t n_query, int d, int kp1, int split_hint,
                              size_t* bytes);
 /* Plan of a call: *ks = 10 * (k-steps of 16) + candidate halves (1: f16 hi only, 2: hi + lo),
- * *list = per-half selection list length, *split = candidate ranges. */
+ * *list = per-half selection list length, *split = candidate ranges; an exhaustive plan
+ * reports *ks = 0, *split = 0 and *list = its block-select capacity. */
 int mepol_knn_plan_info(int64_t n_cand, int64_t n_query, int d, int kp1, int split_hint, int* ks,
                         int* list, int* split);
 int mepol_knn(const float* cand, int64_t n_cand, const float* query, int64_t n_query, int d,
               int kp1, int split_hint, double* dist_out, int64_t* idx_out, int32_t* idx32_out,
               int32_t* n_fallback_out, void* workspace, size_t workspace_bytes, void* stream);
 /* mepol_knn without the host synchronisation: invalid_out (device int32 [2], required) receives
- * [rows with a NaN / inf coordinate, rows whose squared norm overflows f32] in stream order,
- * and when either is nonzero every later kernel of the call returns at once (the outputs are
- * then undefined).  The caller reads invalid_out at its next synchronisation point and raises
- * as mepol_knn would; the epoch path does so once the CSR build is queued behind the k-NN. */
+ * [rows with a NaN / inf coordinate, rows whose squared norm overflows f32] in stream order.
+ * When the first is nonzero every later kernel of the call returns at once (the outputs are
+ * then undefined); the caller reads invalid_out at its next synchronisation point and raises
+ * as mepol_knn would (the epoch path does so once the CSR build is queued behind the k-NN).
+ * The second is informational: such a call is answered by the exhaustive scan. */
 int mepol_knn_deferred(const float* cand, int64_t n_cand, const float* query, int64_t n_query,
                        int d, int kp1, int split_hint, double* dist_out, int64_t* idx_out,
                        int32_t* idx32_out, int32_t* n_fallback_out, int32_t* invalid_out,
                        void* workspace, size_t workspace_bytes, void* stream);
-/* Exhaustive f64 scan for every query (kp1 <= 64); scratch_idx: int32 [1 + n_query]. */
+/* Exhaustive f64 scan for every query, no validation, no workspace (an independent check of
+ * mepol_knn); kp1 <= 3072 (beyond: MEPOL_ERR_UNSUPPORTED, mepol_knn takes any kp1);
+ * scratch_idx is unused (nullable). */
 int mepol_knn_exact(const float* cand, int64_t n_cand, const float* query, int64_t n_query, int d,
                     int kp1, double* dist_out, int64_t* idx_out, int32_t* idx32_out,
                     int32_t* scratch_idx, void* stream);

@@ -325,9 +325,7 @@ def collect_particles_and_compute_knn(env, behavioral_policy, num_traj, traj_len
     real_traj_lengths = rtl32.to(int_type)
     batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T,
                             lengths=lens_host)
-    P.register(I, batch)
-    batch.csr(k)  # queued now: the GPU builds it while the host sets up the off-policy loop
-    check.raise_if_invalid()  # sklearn's check_array ValueError, as kneighbors raises it
+    _register_checked(I, batch, k, check)
     return states, actions, real_traj_lengths, next_states, D, I
 
 
@@ -344,10 +342,21 @@ def make_particle_batch(states, actions, real_traj_lengths, next_states_f32, k,
         knn_events[1].record()
     batch = P.ParticleBatch(states, actions, real_traj_lengths, D, I, idx32T=I32T,
                             lengths=lens_host)
-    P.register(I, batch)
-    batch.csr(k)  # queued now: the GPU builds it while the host sets up the off-policy loop
-    check.raise_if_invalid()
+    _register_checked(I, batch, k, check)
     return states, actions, real_traj_lengths, next_states_f32.to(float_type), D, I
+
+
+def _register_checked(I, batch, k, check):
+    """Register the epoch's batch and queue its CSR build (the GPU builds it while the host
+    sets up the off-policy loop), then read the k-NN's deferred input check: a rejected input
+    (sklearn's check_array ValueError, as kneighbors raises it) leaves no batch registered."""
+    P.register(I, batch)
+    batch.csr(k)
+    try:
+        check.raise_if_invalid()
+    except ValueError:
+        P.unregister(I)
+        raise
 
 
 # ---------------------------------------------------------------------------------------------

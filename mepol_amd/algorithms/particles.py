@@ -105,6 +105,11 @@ def register(indices, batch):
     return batch
 
 
+def unregister(indices):
+    """Drop the batch registered for `indices` (a rejected k-NN input: its D / I are undefined)."""
+    _REGISTRY.pop(id(indices), None)
+
+
 def lookup(states, actions, real_traj_lengths, distances, indices):
     """The registered batch for these tensors, or a new one built from them."""
     b = _REGISTRY.get(id(indices))

@@ -201,38 +201,8 @@ __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X
 // ---------------------------------------------------------------------------------------
 // 3. refine + certify
 // ---------------------------------------------------------------------------------------
-__device__ __forceinline__ bool lex_less(double a, int ai, double b, int bi) {
-  return a < b || (a == b && ai < bi);
-}
 __device__ __forceinline__ bool lex_less_f(float a, int ai, float b, int bi) {
   return a < b || (a == b && ai < bi);
-}
-
-// Exact f64 squared distance, summed in feature order with no contraction (matches the
-// reference's kd_tree rdist: sum of (x_f - y_f)^2 in double, f = 0..d-1).
-// The row is read 32 features at a time with every load issued before the first use (clamped,
-// unconditional addresses): one memory latency per chunk instead of one per feature (the
-// refine's random candidate rows miss L2, and the per-feature loop serialised those misses).
-__device__ __forceinline__ double exact_d2(const float* __restrict__ a, const float* __restrict__ b, int d) {
-  constexpr int kCh = 32;
-  double s = 0.0;
-  for (int f0 = 0; f0 < d; f0 += kCh) {
-    float av[kCh], bv[kCh];
-#pragma unroll
-    for (int u = 0; u < kCh; ++u) {
-      const int f = min(f0 + u, d - 1);
-      av[u] = a[f];
-      bv[u] = b[f];
-    }
-#pragma unroll
-    for (int u = 0; u < kCh; ++u) {
-      if (f0 + u < d) {  // uniform condition
-        const double t = __dsub_rn((double)av[u], (double)bv[u]);
-        s = __dadd_rn(s, __dmul_rn(t, t));
-      }
-    }
-  }
-  return s;
 }
 
 // exact_d2 with b a padded candidate row (16-B aligned, zeros past d, length a multiple of 32):
@@ -257,20 +227,6 @@ __device__ __forceinline__ double exact_d2_pad(const float* __restrict__ a,
     }
   }
   return s;
-}
-
-// Correctly rounded f64 square root (round-to-nearest-even, as glibc / numpy / sklearn).
-// y0 = sqrt(x) is within 1 ulp; with Y = y/ulp(y) an integer, x/ulp^2 is an integer, so
-// "RN(sqrt x) >= y+"  <=>  x > y*y+  and  "RN(sqrt x) <= y-"  <=>  x <= y-*y; both signs are
-// exact through one fma (a rounded nonzero keeps its sign).
-__device__ __forceinline__ double sqrt_rn(double x) {
-  const double y = sqrt(x);
-  if (!(x > 1e-290) || !(x < 1e300)) return y;
-  const double yp = __longlong_as_double(__double_as_longlong(y) + 1);
-  if (__builtin_fma(-y, yp, x) > 0.0) return yp;
-  const double ym = __longlong_as_double(__double_as_longlong(y) - 1);
-  if (__builtin_fma(-ym, y, x) <= 0.0) return ym;
-  return y;
 }
 
 template <int LIST, int MAXP>
@@ -489,212 +445,6 @@ __global__ __launch_bounds__(256) void refine_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// 4. exhaustive exact fallback for uncertified queries
-// ---------------------------------------------------------------------------------------
-// Exhaustive f64 top-kp1 of query xq over candidates [c0, c1), lexicographic (dist, idx):
-// per-thread sorted lists, then kp1 rounds of block argmin; round r's winner goes to
-// emit(r, d, i) on thread 0 (i = INT_MAX, d = inf when the range holds fewer than kp1).
-template <int LIST, typename Emit>
-__device__ __forceinline__ void exact_scan(const float* __restrict__ cand, int64_t c0, int64_t c1,
-                                           const float* __restrict__ xq, int d, int kp1,
-                                           double* red_d, int* red_i, Emit emit) {
-  const int tid = threadIdx.x;
-  const int l = tid & 63, w = tid >> 6;
-  double ld[LIST];
-  int li[LIST];
-#pragma unroll
-  for (int j = 0; j < LIST; ++j) {
-    ld[j] = INFINITY;
-    li[j] = INT_MAX;
-  }
-#pragma nounroll
-  for (int64_t c = c0 + tid; c < c1; c += blockDim.x) {
-    const double x = exact_d2(xq, cand + c * d, d);
-    const int xi = (int)c;
-    if (lex_less(x, xi, ld[LIST - 1], li[LIST - 1])) {
-      bool cc[LIST];
-#pragma unroll
-      for (int j = 0; j < LIST; ++j) cc[j] = lex_less(x, xi, ld[j], li[j]);
-#pragma unroll
-      for (int j = LIST - 1; j >= 1; --j) {
-        ld[j] = cc[j - 1] ? ld[j - 1] : (cc[j] ? x : ld[j]);
-        li[j] = cc[j - 1] ? li[j - 1] : (cc[j] ? xi : li[j]);
-      }
-      ld[0] = cc[0] ? x : ld[0];
-      li[0] = cc[0] ? xi : li[0];
-    }
-  }
-#pragma nounroll
-  for (int r = 0; r < kp1; ++r) {
-    double bd = ld[0];
-    int bi = li[0];
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      const double od = __shfl_xor(bd, m, kWave);
-      const int oi = __shfl_xor(bi, m, kWave);
-      if (lex_less(od, oi, bd, bi)) {
-        bd = od;
-        bi = oi;
-      }
-    }
-    if (l == 0) {
-      red_d[w] = bd;
-      red_i[w] = bi;
-    }
-    __syncthreads();
-    bd = red_d[0];
-    bi = red_i[0];
-#pragma unroll
-    for (int u = 1; u < 4; ++u)
-      if (lex_less(red_d[u], red_i[u], bd, bi)) {
-        bd = red_d[u];
-        bi = red_i[u];
-      }
-    __syncthreads();
-    if (li[0] == bi && bi != INT_MAX) {
-#pragma unroll
-      for (int j = 0; j < LIST - 1; ++j) {
-        ld[j] = ld[j + 1];
-        li[j] = li[j + 1];
-      }
-      ld[LIST - 1] = INFINITY;
-      li[LIST - 1] = INT_MAX;
-    }
-    if (tid == 0) emit(r, bd, bi);
-  }
-}
-
-// Queued (uncertified) queries.  With fewer queries than blocks each query's candidates are cut
-// into nchunk = grid / count ranges, one block each (partial top-kp1 lists to part_*, merged by
-// exact_merge_kernel): a handful of queries then use the whole chip instead of one CU each.
-// With part_d == nullptr or count >= grid, a block answers whole queries.
-__host__ __device__ inline int exact_nchunk(int count, int grid) {
-  return (count <= 0 || count >= grid) ? 1 : grid / count;
-}
-
-template <int LIST>
-__global__ __launch_bounds__(256) void exact_kernel(const float* __restrict__ cand, int64_t nc,
-                                                    const float* __restrict__ query, int64_t nq,
-                                                    int d, int kp1,
-                                                    const int* __restrict__ flag_count,
-                                                    const int* __restrict__ flag_list,
-                                                    double* __restrict__ Dout,
-                                                    int64_t* __restrict__ I64,
-                                                    int32_t* __restrict__ I32,
-                                                    double* __restrict__ part_d,
-                                                    int* __restrict__ part_i) {
-  __shared__ double red_d[4];
-  __shared__ int red_i[4];
-  const int count = *flag_count;
-  const int nchunk = part_d ? exact_nchunk(count, (int)gridDim.x) : 1;
-  if (nchunk == 1) {
-    for (int fi = blockIdx.x; fi < count; fi += gridDim.x) {
-      const int64_t q = flag_list[fi];
-      exact_scan<LIST>(cand, 0, nc, query + q * d, d, kp1, red_d, red_i,
-                       [&](int r, double bd, int bi) {
-                         Dout[q * kp1 + r] = sqrt_rn(bd);
-                         if (I64) I64[q * kp1 + r] = bi;
-                         if (I32) I32[(int64_t)r * nq + q] = bi;  // transposed [kp1][nq]
-                       });
-    }
-    return;
-  }
-  const int fi = (int)blockIdx.x / nchunk, ch = (int)blockIdx.x % nchunk;
-  if (fi >= count) return;
-  const int64_t q = flag_list[fi];
-  const int64_t c0 = nc * ch / nchunk, c1 = nc * (ch + 1) / nchunk;
-  const int64_t o = ((int64_t)fi * nchunk + ch) * kp1;
-  exact_scan<LIST>(cand, c0, c1, query + q * d, d, kp1, red_d, red_i,
-                   [&](int r, double bd, int bi) {
-                     part_d[o + r] = bd;
-                     part_i[o + r] = bi;
-                   });
-}
-
-// Merge of the nchunk sorted partial lists of one queued query (exact_kernel, chunked form):
-// kp1 rounds of block argmin over the list heads; grid = the exact kernel's grid.
-__global__ __launch_bounds__(256) void exact_merge_kernel(int grid, int kp1, int64_t nq,
-                                                          const int* __restrict__ flag_count,
-                                                          const int* __restrict__ flag_list,
-                                                          const double* __restrict__ part_d,
-                                                          const int* __restrict__ part_i,
-                                                          double* __restrict__ Dout,
-                                                          int64_t* __restrict__ I64,
-                                                          int32_t* __restrict__ I32) {
-  __shared__ double red_d[4];
-  __shared__ int red_i[4];
-  __shared__ int red_t[4];
-  const int count = *flag_count;
-  const int nchunk = exact_nchunk(count, grid);
-  const int fi = blockIdx.x;
-  if (nchunk == 1 || fi >= count) return;
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-  const int64_t q = flag_list[fi];
-  const int64_t base = (int64_t)fi * nchunk * kp1;
-  constexpr int kPer = 2;  // lists per thread: nchunk <= grid <= 512
-  int pos[kPer] = {0, 0};
-  for (int r = 0; r < kp1; ++r) {
-    double bd = INFINITY;
-    int bi = INT_MAX, bt = -1;
-#pragma unroll
-    for (int u = 0; u < kPer; ++u) {
-      const int ch = tid + u * 256;
-      if (ch < nchunk && pos[u] < kp1) {
-        const double x = part_d[base + (int64_t)ch * kp1 + pos[u]];
-        const int xi = part_i[base + (int64_t)ch * kp1 + pos[u]];
-        if (lex_less(x, xi, bd, bi)) {
-          bd = x;
-          bi = xi;
-          bt = u;
-        }
-      }
-    }
-    int owner = bt >= 0 ? tid * kPer + bt : INT_MAX;  // which (thread, list) holds the winner
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-      const double od = __shfl_xor(bd, m, kWave);
-      const int oi = __shfl_xor(bi, m, kWave);
-      const int ot = __shfl_xor(owner, m, kWave);
-      if (lex_less(od, oi, bd, bi) || (od == bd && oi == bi && ot < owner)) {
-        bd = od;
-        bi = oi;
-        owner = ot;
-      }
-    }
-    if (l == 0) {
-      red_d[w] = bd;
-      red_i[w] = bi;
-      red_t[w] = owner;
-    }
-    __syncthreads();
-    bd = red_d[0];
-    bi = red_i[0];
-    owner = red_t[0];
-#pragma unroll
-    for (int u = 1; u < 4; ++u)
-      if (lex_less(red_d[u], red_i[u], bd, bi) ||
-          (red_d[u] == bd && red_i[u] == bi && red_t[u] < owner)) {
-        bd = red_d[u];
-        bi = red_i[u];
-        owner = red_t[u];
-      }
-    __syncthreads();
-    if (owner != INT_MAX && owner / kPer == tid) ++pos[owner % kPer];
-    if (tid == 0) {
-      Dout[q * kp1 + r] = sqrt_rn(bd);
-      if (I64) I64[q * kp1 + r] = bi;
-      if (I32) I32[(int64_t)r * nq + q] = bi;  // transposed [kp1][nq]
-    }
-  }
-}
-
-__global__ void fill_identity_kernel(int* s, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i == 0) s[0] = (int)n;
-  if (i < n) s[1 + i] = (int)i;
-}
-
-// ---------------------------------------------------------------------------------------
 // host-side plan + dispatch
 // ---------------------------------------------------------------------------------------
 struct Plan {
@@ -707,8 +457,35 @@ struct Plan {
   int LIST16;     // per-half select list length
   int M;          // refine input entries per query: 2*split*LIST16
   int64_t nc, nq, nct, nqt, tiles_per_split;
-  size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_part, off_cpad, off_seed, total;
+  bool exhaustive;  // no f16 screen: every query scanned exactly (knn_exact.hip block select)
+  size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_part, off_cpad, off_seed;
+  size_t off_candT, off_wbuf, total;
 };
+
+// The f16 screen (select + refine) covers d <= kScreenMaxD (4 k-steps of 16 with the norm
+// column) and k + 1 <= kScreenMaxKp1 (two half lists of <= 40 behind the union bound, refine's
+// 64 ranked entries); every other shape takes the exhaustive plan.
+constexpr int kScreenMaxD = 63;
+constexpr int kScreenMaxKp1 = 60;
+
+// Exhaustive plan: validation scalars, the transposed candidates and (kp1 beyond the LDS
+// capacity) the block-select buffers.
+static int make_exhaustive_plan(Plan* P) {
+  size_t off = 0;
+  P->exhaustive = true;
+  P->split = 0;
+  P->LIST16 = wide_cap(P->kp1);
+  P->KS16 = 0;
+  P->nh = 0;
+  P->off_scalars = off;
+  off = align_up(off + 32, 256);
+  P->off_candT = off;
+  off = align_up(off + (size_t)P->nc * P->d * sizeof(float), 256);
+  P->off_wbuf = off;
+  off = align_up(off + wide_buffer_bytes(P->nq, 1, P->kp1), 256);
+  P->total = off;
+  return 0;
+}
 
 static const int kListChoices[] = {8, 16, 22, 24, 32, 40};  // 22 = keep + 4 at k + 1 = 31
 
@@ -727,25 +504,20 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
     set_error("mepol_knn: n_cand=%lld exceeds int32 indexing", (long long)nc);
     return kErrUnsupported;
   }
-  if (d > 63 || kp1 > 60) {
-    set_error("mepol_knn: unsupported d=%d / k+1=%d (fast path supports d<=63, k+1<=60; "
-              "mepol_knn_exact covers the rest)", d, kp1);
-    return kErrUnsupported;
-  }
   P->d = d;
   P->kp1 = kp1;
+  P->nc = nc;
+  P->nq = nq;
+  P->exhaustive = false;
+  if (d > kScreenMaxD || kp1 > kScreenMaxKp1) return make_exhaustive_plan(P);
   P->KS16 = (d + 1 + 15) / 16;
   // f16 lists: each half-lane keeps LIST16 entries and prunes against the union bound
   // (flush_buffer, keep = ceil(kp1/2) + 2 per half: 2 keep >= kp1 + 3).  A half holding more
   // than LIST16 of the query's nearest candidates only costs certification (exact path).
   P->keep = (kp1 + 1) / 2 + 2;
   P->LIST16 = 40;
-  static const bool no22 = [] {  // MEPOL_KNN_LIST22=0: skip the 22-entry lists (A/B probe)
-    const char* e = getenv("MEPOL_KNN_LIST22");
-    return e && e[0] == '0';
-  }();
   for (int v : kListChoices)
-    if (v >= P->keep + 4 && !(no22 && v == 22)) {
+    if (v >= P->keep + 4) {
       P->LIST16 = v;
       break;
     }
@@ -781,8 +553,6 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   // the selection's error band (~0.1 at C3) holds a few more candidates around the (k+1)-th
   // than kp1 + 4: refine ranks the approximate top 64 and evaluates those inside the band
   P->LIST = kRefineList;
-  P->nc = nc;
-  P->nq = nq;
   P->nct = (nc + 31) / 32;
   P->nqt = (nq + 31) / 32;
   int split = split_hint;
@@ -829,28 +599,22 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   off = align_up(off + (size_t)nc * P->dp * sizeof(float), 256);
   P->off_seed = off;  // per-query prune-bound seeds (select16_kernel)
   off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(int), 256);
+  P->off_candT = P->off_wbuf = 0;
   P->total = off;
   return 0;
 }
 
-// MEPOL_KNN_SEED=0: every candidate range starts its prune bound at +inf (A/B probe).
+// MEPOL_KNN_SEED=0: every candidate range starts its prune bound at +inf.  The certified
+// output is the same bits either way (tests/test_gpu_knn.py::test_knn_seed_invariance); only
+// the partial lists, and so the count of queries sent to the exhaustive stage, differ.
 static int select_seed() {
-  static const int v = [] {
-    const char* e = getenv("MEPOL_KNN_SEED");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return v;
+  const char* e = getenv("MEPOL_KNN_SEED");
+  return (e && e[0] == '0') ? 0 : 1;
 }
 
-// refine_kernel's merge of the partial lists: 2 = per-list binary-search ranks (default),
-// 1 = ranks counted against every entry, 0 = argmin rounds (MEPOL_KNN_RANK_MERGE, A/B probe).
-static int refine_rank_merge() {
-  static const int v = [] {
-    const char* e = getenv("MEPOL_KNN_RANK_MERGE");
-    return e ? atoi(e) : 2;
-  }();
-  return v;
-}
+// refine_kernel's merge of the partial lists: per-list binary-search ranks (2); the kernel
+// keeps the full-count ranks (1) and argmin rounds (0) for MAXP > 4 plans.
+constexpr int kRankMerge = 2;
 
 static void launch_refine(const Plan& P, const float* cpad, const float* query, const float* lv,
                           const int* li, const unsigned* cmax, double* D, int64_t* I64,
@@ -860,7 +624,7 @@ static void launch_refine(const Plan& P, const float* cpad, const float* query, 
 #define MEPOL_REFINE(MP)                                                                          \
   hipLaunchKernelGGL((refine_kernel<kRefineList, MP>), g, dim3(256), 0, st, cpad, P.dp, P.nc,     \
                      query, P.nq, P.d, P.kp1, P.M, P.LIST16, lv, li, cmax, P.e_terms, D, I64,     \
-                     I32, fc, fl, refine_rank_merge())
+                     I32, fc, fl, kRankMerge)
   if (P.maxp <= 2)
     MEPOL_REFINE(2);
   else if (P.maxp <= 4)
@@ -872,39 +636,6 @@ static void launch_refine(const Plan& P, const float* cpad, const float* query, 
   else
     MEPOL_REFINE(32);
 #undef MEPOL_REFINE
-}
-
-template <int LIST>
-static void launch_exact_list(const Plan& P, const float* cand, const float* query, const int* fc,
-                              const int* fl, double* D, int64_t* I64, int32_t* I32,
-                              unsigned grid, hipStream_t st, double* part_d = nullptr,
-                              int* part_i = nullptr) {
-  hipLaunchKernelGGL((exact_kernel<LIST>), dim3(grid), dim3(256), 0, st, cand, P.nc, query, P.nq,
-                     P.d, P.kp1, fc, fl, D, I64, I32, part_d, part_i);
-  if (part_d)
-    hipLaunchKernelGGL(exact_merge_kernel, dim3(grid), dim3(256), 0, st, (int)grid, P.kp1, P.nq,
-                       fc, fl, part_d, part_i, D, I64, I32);
-}
-
-template <int LIST>
-static void launch_exact(const Plan& P, const float* cand, const float* query, const int* fc,
-                         const int* fl, double* D, int64_t* I64, int32_t* I32, unsigned grid,
-                         hipStream_t st, double* part_d, int* part_i) {
-  launch_exact_list<LIST>(P, cand, query, fc, fl, D, I64, I32, grid, st, part_d, part_i);
-}
-
-static void launch_exact_kp1(const Plan& P, const float* cand, const float* query, const int* fc,
-                             const int* fl, double* D, int64_t* I64, int32_t* I32, unsigned grid,
-                             hipStream_t st, double* part_d, int* part_i) {
-  // per-thread list >= kp1 (kp1 <= 64)
-  if (P.kp1 <= 8)
-    launch_exact<8>(P, cand, query, fc, fl, D, I64, I32, grid, st, part_d, part_i);
-  else if (P.kp1 <= 16)
-    launch_exact<16>(P, cand, query, fc, fl, D, I64, I32, grid, st, part_d, part_i);
-  else if (P.kp1 <= 40)
-    launch_exact<40>(P, cand, query, fc, fl, D, I64, I32, grid, st, part_d, part_i);
-  else
-    launch_exact<64>(P, cand, query, fc, fl, D, I64, I32, grid, st, part_d, part_i);
 }
 
 }  // namespace knn
@@ -954,34 +685,39 @@ static int knn_impl(const float* cand, int64_t n_cand, const float* query, int64
   if (n_query == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
   char* ws = (char*)workspace;
-  _Float16* ap16 = (_Float16*)(ws + P.off_apack);
   unsigned* cmax = (unsigned*)(ws + P.off_scalars);
   int* fcount = n_fallback_out ? (int*)n_fallback_out : (int*)(ws + P.off_scalars + 4);
-  float* lv = (float*)(ws + P.off_lv);
-  int* li = (int*)(ws + P.off_li);
-  int* flist = (int*)(ws + P.off_flag);
-  double* pd = (double*)(ws + P.off_part);
-  int* pi = (int*)(ws + P.off_part + (size_t)kExactGrid * 64 * sizeof(double));
-  float* cpad = (float*)(ws + P.off_cpad);
   MEPOL_HIP(hipMemsetAsync(ws + P.off_scalars, 0, 32, st));
   if (n_fallback_out) MEPOL_HIP(hipMemsetAsync(n_fallback_out, 0, sizeof(int32_t), st));
-  // scal[0] = max candidate norm (refine's C), scal[2] = max query norm (f16 scale)
   const bool self_query = query == cand && P.nq == P.nc;
-  const size_t stage_lds = (size_t)kStageRows * P.d * sizeof(float);  // <= 32 KB (d <= 63)
-  auto norms_grid = [](int64_t rows) {
-    return dim3((unsigned)std::min<int64_t>(kNormsBlocks, (rows + kStageRows - 1) / kStageRows));
-  };
-  hipLaunchKernelGGL(norms_kernel, norms_grid(P.nc), dim3(kNormsThreads), stage_lds, st, cand,
-                     P.nc, P.d, cmax, cmax + 4, self_query ? cmax + 2 : nullptr);
-  if (!self_query)
-    hipLaunchKernelGGL(norms_kernel, norms_grid(P.nq), dim3(kNormsThreads), stage_lds, st, query,
-                       P.nq, P.d, cmax + 2, cmax + 4, nullptr);
+  ExactArgs ea{cand,     nullptr,  P.nc,    query,  P.nq,    P.d,     P.kp1,   fcount,
+               nullptr,  cmax,     0,       dist_out, idx_out, idx32_out, nullptr, nullptr,
+               nullptr,  nullptr};
+  // 0. validation (+ the transposed candidates of an exhaustive plan)
+  if (P.exhaustive) {
+    ea.candT = (float*)(ws + P.off_candT);
+    launch_transpose_validate(cand, P.nc, P.d, (float*)ea.candT, cmax + 4, st);
+    if (!self_query) launch_transpose_validate(query, P.nq, P.d, nullptr, cmax + 4, st);
+  } else {
+    // scal[0] = max candidate norm (refine's C), scal[2] = max query norm (f16 scale)
+    const size_t stage_lds = (size_t)kStageRows * P.d * sizeof(float);  // <= 32 KB (d <= 63)
+    auto norms_grid = [](int64_t rows) {
+      return dim3((unsigned)std::min<int64_t>(kNormsBlocks, (rows + kStageRows - 1) / kStageRows));
+    };
+    hipLaunchKernelGGL(norms_kernel, norms_grid(P.nc), dim3(kNormsThreads), stage_lds, st, cand,
+                       P.nc, P.d, cmax, cmax + 4, self_query ? cmax + 2 : nullptr);
+    if (!self_query)
+      hipLaunchKernelGGL(norms_kernel, norms_grid(P.nq), dim3(kNormsThreads), stage_lds, st,
+                         query, P.nq, P.d, cmax + 2, cmax + 4, nullptr);
+  }
   MEPOL_CHECK_LAUNCH();
   if (invalid_out) {
     MEPOL_HIP(hipMemcpyAsync(invalid_out, cmax + 4, 2 * sizeof(int32_t), hipMemcpyDeviceToDevice,
                              st));
   } else {
     // sklearn rejects non-finite input (ValueError from check_array): validate before the scan.
+    // Rows whose f32 squared norm overflows (bad[1]) are valid input: the f16 screen cannot
+    // scale them, so every query goes to the exhaustive f64 stage (ExactArgs).
     unsigned bad[2] = {0, 0};
     MEPOL_HIP(hipMemcpyAsync(bad, cmax + 4, sizeof(bad), hipMemcpyDeviceToHost, st));
     MEPOL_HIP(hipStreamSynchronize(st));
@@ -989,11 +725,23 @@ static int knn_impl(const float* cand, int64_t n_cand, const float* query, int64
       set_error("mepol_knn: Input contains NaN or infinity (%u rows)", bad[0]);
       return kErrBadArg;
     }
-    if (bad[1]) {
-      set_error("mepol_knn: %u rows have a squared norm beyond float32 range", bad[1]);
-      return kErrUnsupported;
-    }
   }
+  if (P.exhaustive) {
+    ea.all = 1;
+    ea.wbuf_d = (double*)(ws + P.off_wbuf);
+    ea.wbuf_i = (int*)(ws + P.off_wbuf +
+                       (size_t)wide_grid(P.nq, 1, P.kp1) * wide_cap(P.kp1) * sizeof(double));
+    if (n_fallback_out)
+      MEPOL_HIP(hipMemsetD32Async((hipDeviceptr_t)n_fallback_out, (int)P.nq, 1, st));
+    launch_exact_stage(ea, st);
+    MEPOL_CHECK_LAUNCH();
+    return 0;
+  }
+  _Float16* ap16 = (_Float16*)(ws + P.off_apack);
+  float* lv = (float*)(ws + P.off_lv);
+  int* li = (int*)(ws + P.off_li);
+  float* cpad = (float*)(ws + P.off_cpad);
+  const size_t stage_lds = (size_t)kStageRows * P.d * sizeof(float);
   hipLaunchKernelGGL(pack16_kernel, dim3((unsigned)((P.nct + 3) / 4)), dim3(256), stage_lds, st,
                      cand, P.nc, P.d, P.KS16, P.nh, P.nct, ap16, cmax, cpad, P.dp);
   MEPOL_CHECK_LAUNCH();
@@ -1013,10 +761,14 @@ static int knn_impl(const float* cand, int64_t n_cand, const float* query, int64
     }
   }
   MEPOL_CHECK_LAUNCH();
+  int* flist = (int*)(ws + P.off_flag);
   launch_refine(P, cpad, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st);
   MEPOL_CHECK_LAUNCH();
-  launch_exact_kp1(P, cand, query, fcount, flist, dist_out, idx_out, idx32_out, kExactGrid, st,
-                   pd, pi);
+  // 4. queued queries (or all of them, scal[5]) by the exhaustive stage
+  ea.flag_list = flist;
+  ea.part_d = (double*)(ws + P.off_part);
+  ea.part_i = (int*)(ws + P.off_part + (size_t)kExactGrid * 64 * sizeof(double));
+  launch_exact_stage(ea, st);
   MEPOL_CHECK_LAUNCH();
   return 0;
 }
@@ -1042,36 +794,31 @@ extern "C" int mepol_knn_deferred(const float* cand, int64_t n_cand, const float
                   n_fallback_out, invalid_out, workspace, workspace_bytes, stream);
 }
 
-// Exhaustive exact k-NN for every query (no f16 selection): the reference semantics at the
-// cost of a full f64 scan.  Used for d > 63 / k+1 > 60 and as an independent check.
+// Exhaustive exact k-NN for every query (no f16 screen, no validation, no workspace): the
+// reference semantics at the cost of a full f64 scan over row-major candidates; an independent
+// check of mepol_knn.  kp1 <= 3072 (its block-select lists live in LDS); scratch_idx is unused
+// (kept for the ABI).
 extern "C" int mepol_knn_exact(const float* cand, int64_t n_cand, const float* query,
                                int64_t n_query, int d, int kp1, double* dist_out, int64_t* idx_out,
                                int32_t* idx32_out, int32_t* scratch_idx, void* stream) {
-  if (n_cand <= 0 || n_query < 0 || d <= 0 || kp1 <= 0 || kp1 > 64 || kp1 > n_cand ||
-      !scratch_idx) {
-    set_error("mepol_knn_exact: bad arguments (needs k+1 <= 64, k+1 <= n_cand, scratch)");
+  (void)scratch_idx;
+  if (n_cand <= 0 || n_query < 0 || d <= 0 || kp1 <= 0 || kp1 > n_cand || !cand || !query ||
+      !dist_out) {
+    set_error("mepol_knn_exact: bad arguments (needs 0 < k+1 <= n_cand)");
     return kErrBadArg;
   }
+  if (n_cand > INT_MAX - 64) {
+    set_error("mepol_knn_exact: n_cand=%lld exceeds int32 indexing", (long long)n_cand);
+    return kErrUnsupported;
+  }
+  if (wide_buffer_bytes(n_query, 1, kp1) > 0) {
+    set_error("mepol_knn_exact: k+1=%d beyond its LDS lists (mepol_knn takes any k+1)", kp1);
+    return kErrUnsupported;
+  }
   if (n_query == 0) return 0;
-  hipStream_t st = (hipStream_t)stream;
-  // scratch_idx: [1 + n_query] int32: count, then the identity query list.
-  Plan P{};
-  P.nc = n_cand;
-  P.nq = n_query;
-  P.d = d;
-  P.kp1 = kp1;
-  hipLaunchKernelGGL(fill_identity_kernel, dim3((unsigned)((n_query + 255) / 256)), dim3(256), 0, st, scratch_idx,
-                     n_query);
-  MEPOL_CHECK_LAUNCH();
-  const unsigned grid = (unsigned)std::min<int64_t>(n_query, 4096);
-  if (kp1 <= 8)
-    launch_exact_list<8>(P, cand, query, scratch_idx, scratch_idx + 1, dist_out, idx_out, idx32_out, grid, st);
-  else if (kp1 <= 16)
-    launch_exact_list<16>(P, cand, query, scratch_idx, scratch_idx + 1, dist_out, idx_out, idx32_out, grid, st);
-  else if (kp1 <= 40)
-    launch_exact_list<40>(P, cand, query, scratch_idx, scratch_idx + 1, dist_out, idx_out, idx32_out, grid, st);
-  else
-    launch_exact_list<64>(P, cand, query, scratch_idx, scratch_idx + 1, dist_out, idx_out, idx32_out, grid, st);
+  const ExactArgs ea{cand, nullptr, n_cand, query, n_query, d, kp1, nullptr, nullptr, nullptr, 1,
+                     dist_out, idx_out, idx32_out, nullptr, nullptr, nullptr, nullptr};
+  launch_exact_stage(ea, (hipStream_t)stream);
   MEPOL_CHECK_LAUNCH();
   return 0;
 }

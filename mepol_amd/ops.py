@@ -5,7 +5,6 @@ must live on a ROCm device; dtypes follow the reference (f64 values, int64 indic
 API boundary; int32 indices internally).
 """
 import math
-import os
 
 import torch
 
@@ -78,12 +77,21 @@ def knn_plan(n_cand, n_query, d, kp1, split=0):
     ks, lst, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
     call("mepol_knn_plan_info", n_cand, n_query, d, kp1, split, ctypes.byref(ks),
          ctypes.byref(lst), ctypes.byref(sp))
-    return {"KS16": ks.value // 10, "nh": ks.value % 10, "LIST16": lst.value, "split": sp.value}
+    # ks == 0: no f16 screen (d > 63 or k+1 > 60): every query takes the exhaustive f64 scan,
+    # LIST16 is then its block-select capacity
+    KS16, nh = ks.value // 10, ks.value % 10
+    # MFMA products per k-step and tile (csrc/knn_select.hpp, select16_kernel: A_hi x q_hi, plus
+    # A_hi x q_lo when kQueryLo = nh == 2 or KS16 >= 4, plus A_lo x q_hi when nh == 2)
+    products = 0 if not ks.value else (3 if nh == 2 else (2 if KS16 >= 4 else 1))
+    return {"mode": "screened" if ks.value else "exhaustive", "KS16": KS16, "nh": nh,
+            "LIST16": lst.value, "split": sp.value, "mfma_products": products}
 
 
-class _NoCheck:
-    def raise_if_invalid(self):
-        pass
+def knn_issued_mfma_flops(n_cand, n_query, plan):
+    """Flops the f16 selection issues on the matrix cores: products x 2 K (K = 16 KS16) per
+    32 x 32 tile pair, padded tiles included."""
+    tiles = -(-n_query // 32) * -(-n_cand // 32)
+    return float(plan["mfma_products"]) * 2 * 16 * plan["KS16"] * 1024 * tiles
 
 
 class KnnInputCheck:
@@ -91,35 +99,60 @@ class KnnInputCheck:
     on the device, copied to pinned host memory in stream order; raise_if_invalid() waits for
     that copy only and raises what mepol_knn would have raised."""
 
-    _pinned = []  # reused pinned slots (a pinned allocation per call cost ~1 ms of host time)
-    _next = 0
+    # Free pinned slots (a pinned allocation per call cost ~1 ms of host time).  A check holds
+    # its slot until raise_if_invalid() has read it (or it is collected); with every slot held
+    # a new one is allocated, so no check can read another call's counts.
+    _free = []
+    _lock = None
 
     def __init__(self, invalid_dev):
+        import threading
+
         cls = KnnInputCheck
-        if not cls._pinned:
-            cls._pinned = [torch.empty(2, dtype=torch.int32, pin_memory=True) for _ in range(8)]
-        self._host = cls._pinned[cls._next]
-        cls._next = (cls._next + 1) % len(cls._pinned)
+        if cls._lock is None:
+            cls._lock = threading.Lock()
+        with cls._lock:
+            slot = cls._free.pop() if cls._free else None
+        self._host = slot if slot is not None else torch.empty(2, dtype=torch.int32,
+                                                               pin_memory=True)
         memcpy_async(self._host, invalid_dev)
         self._event = torch.cuda.Event()
         self._event.record(torch.cuda.current_stream(invalid_dev.device))
         self._dev = invalid_dev
+        self._nonfinite = 0
 
     def raise_if_invalid(self):
-        from ._lib import MepolError, MepolInputError
+        """Raises sklearn's ValueError for a NaN / inf coordinate.  The second count (rows whose
+        f32 squared norm overflows) is not an error: those calls were answered by the
+        exhaustive f64 scan."""
+        from ._lib import MepolInputError
 
-        self._event.synchronize()
-        nonfinite, overflow = (int(x) for x in self._host.tolist())
-        if nonfinite:
+        if self._host is not None:
+            self._event.synchronize()
+            self._nonfinite = int(self._host[0])
+            self._release()
+        if self._nonfinite:
             raise MepolInputError(f"mepol_knn failed (rc=1001): mepol_knn: Input contains NaN or "
-                                  f"infinity ({nonfinite} rows)")
-        if overflow:
-            raise MepolError(f"mepol_knn failed (rc=1003): mepol_knn: {overflow} rows have a "
-                             "squared norm beyond float32 range")
+                                  f"infinity ({self._nonfinite} rows)")
+
+    def _release(self):
+        """Returns the slot once its copy has landed (never while the copy may still write)."""
+        host, self._host = getattr(self, "_host", None), None
+        if host is not None:
+            self._event.synchronize()
+            with KnnInputCheck._lock:
+                KnnInputCheck._free.append(host)
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:
+            pass
 
 
 def knn(cand, kp1, query=None, split=0, want_int64=True, return_fallback=False, defer_check=False):
-    """Exact k-NN of `query` rows among `cand` rows (both f32 [*, d] on device).
+    """Exact k-NN of `query` rows among `cand` rows (both f32 [*, d] on device), any d and any
+    kp1 <= len(cand) (sklearn raises beyond, and so does this: MepolInputError).
 
     Returns (D f64 [nq, kp1], I int64 [nq, kp1] or None, I32T int32 [kp1, nq]) and, with
     return_fallback, the device int32 count of queries that took the exhaustive path.
@@ -147,10 +180,6 @@ def knn(cand, kp1, query=None, split=0, want_int64=True, return_fallback=False, 
     I32T = torch.empty((kp1, nq), dtype=torch.int32, device=dev)
     nfb = torch.zeros(1, dtype=torch.int32, device=dev)
     out = (D, I, I32T) + ((nfb,) if return_fallback else ())
-    if defer_check and os.environ.get("MEPOL_KNN_SYNC_CHECK") == "1":  # A/B probe
-        call("mepol_knn", ptr(cand), nc, ptr(query), nq, d, kp1, split, ptr(D), ptr(I), ptr(I32T),
-             ptr(nfb), ptr(ws), ws.numel(), _stream())
-        return out + (_NoCheck(),)
     if defer_check:
         invalid = torch.empty(2, dtype=torch.int32, device=dev)
         call("mepol_knn_deferred", ptr(cand), nc, ptr(query), nq, d, kp1, split, ptr(D), ptr(I),
@@ -162,7 +191,8 @@ def knn(cand, kp1, query=None, split=0, want_int64=True, return_fallback=False, 
 
 
 def knn_exact(cand, kp1, query=None, want_int64=True):
-    """Exhaustive f64 k-NN (every query scanned exactly); reference semantics, slower."""
+    """Exhaustive f64 k-NN (every query scanned exactly, no input validation); reference
+    semantics, slower: the independent check of knn().  kp1 <= 3072."""
     if query is None:
         query = cand
     _require_device(cand, query)
@@ -174,9 +204,8 @@ def knn_exact(cand, kp1, query=None, want_int64=True):
     D = torch.empty((nq, kp1), dtype=torch.float64, device=dev)
     I = torch.empty((nq, kp1), dtype=torch.int64, device=dev) if want_int64 else None
     I32T = torch.empty((kp1, nq), dtype=torch.int32, device=dev)
-    scratch = torch.empty(nq + 1, dtype=torch.int32, device=dev)
     call("mepol_knn_exact", ptr(cand), nc, ptr(query), nq, d, kp1, ptr(D), ptr(I), ptr(I32T),
-         ptr(scratch), _stream())
+         None, _stream())
     return D, I, I32T
 
 

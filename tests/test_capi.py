@@ -50,7 +50,15 @@ def test_bad_arguments_fail_loudly_without_gpu():
     rc = lib.mepol_knn_workspace_size(10, 10, 3, 50, 0, ctypes.byref(n))  # k+1 > n
     assert rc == 1001
     assert b"n_neighbors" in lib.mepol_last_error_string()
-    rc = lib.mepol_knn_workspace_size(1000, 1000, 200, 5, 0, ctypes.byref(n))  # d too large
+    # any d and any k+1 <= n have a plan (the exhaustive one beyond the f16 screen's shapes)
+    for nn, d, kp1 in [(1000, 200, 5), (1000, 29, 101), (1000, 3, 1000)]:
+        rc = lib.mepol_knn_workspace_size(nn, nn, d, kp1, 0, ctypes.byref(n))
+        assert rc == 0 and n.value >= nn * d * 4
+        ks, lst, sp = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        assert lib.mepol_knn_plan_info(nn, nn, d, kp1, 0, ctypes.byref(ks), ctypes.byref(lst),
+                                       ctypes.byref(sp)) == 0
+        assert ks.value == 0 and lst.value >= kp1
+    rc = lib.mepol_knn_workspace_size(2 ** 31, 10, 3, 5, 0, ctypes.byref(n))  # int32 indices
     assert rc == 1003
     rc = lib.mepol_knn_workspace_size(200000, 200000, 29, 31, 0, ctypes.byref(n))
     assert rc == 0 and n.value > 200000 * 31 * 8

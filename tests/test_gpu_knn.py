@@ -225,3 +225,22 @@ def test_knn_exact_chunked_few_queries(cuda, nq):
     Do, Io = O.knn_exact(X, 51, Q=Q)
     assert np.array_equal(D.cpu().numpy(), Do) and np.array_equal(I.cpu().numpy(), Io)
 
+
+
+def test_knn_seed_invariance(cuda, monkeypatch):
+    """The cross-range bound seed changes which candidates the partial lists keep (and so how
+    many queries refine certifies), never the certified output: D / I with the seed on and off
+    are the same bits, on fallback-heavy duplicate clusters and on Ant-shaped data."""
+    rng = np.random.default_rng(7)
+    base = rng.standard_normal((40, 12)).astype(np.float32)
+    Xdup = np.repeat(base, 100, axis=0)
+    Xdup[::5] += np.float32(1e-6) * rng.standard_normal((len(Xdup[::5]), 12)).astype(np.float32)
+    Xant = rng.standard_normal((6000, 29)).astype(np.float32)
+    for X, kp1 in ((Xdup, 31), (Xant, 31)):
+        monkeypatch.setenv("MEPOL_KNN_SEED", "1")
+        D1, I1, _, _ = _knn(X, kp1, split=3)
+        monkeypatch.setenv("MEPOL_KNN_SEED", "0")
+        D0, I0, _, _ = _knn(X, kp1, split=3)
+        assert np.array_equal(D1, D0) and np.array_equal(I1, I0)
+        Do, Io = O.knn_exact(X, kp1)
+        assert np.array_equal(D1, Do) and np.array_equal(I1, Io)
