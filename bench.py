@@ -503,7 +503,7 @@ def knn_source_stamp():
 
 
 PEAK_F64_TFLOPS = 78.6            # MI355X spec: FP64 matrix (dense)
-MEASURED_F64_MFMA_TFLOPS = 49.6   # tools/f64_rate_probe.hip: v_mfma_f64_16x16x4, 8 chains
+MEASURED_F64_MFMA_TFLOPS = 77.9   # tools/f64_mfma_table.hip (profiles/r5/f64/): 16x16x4, >= 2 waves/SIMD
 
 
 def _mlp_roofline(it):

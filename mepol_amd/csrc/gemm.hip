@@ -202,19 +202,39 @@ __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
   d4 acc[FR][FC];
   gemm_mainloop<WR, WC, FR, FC>(dz2, N, K, K, W2t, M, K, row0, col0, lds, acc);
 
+  // Every epilogue operand in ONE batch of unconditional loads (clamped addresses) before the
+  // first use: the ReLU mask of h1 at the wave's accumulator elements and the [x | 1] operands.
+  // Loaded where they were used, the h1 loads waited out their HBM latency in FC batches
+  // (0.40 of the kernel's 1.23 ms went to this epilogue, profiles/r5/f64/).
   // B operands [x | 1] for k-step (i, q): lane (fr, g) holds x[row(i, q, g)][16 h + fr]
   double xb[FR][4][NH];
+  double hv[FC][FR][4];
 #pragma unroll
   for (int i = 0; i < FR; ++i)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+      // accumulator element (row g + 4 q of fragment i, col fr) is A[m = fr][k = g] of
+      // k-step (i, q): rows 16 i + 4 q + g
       const int64_t r = row0 + wave * FR * 16 + i * 16 + 4 * q + g;
       const double* xr = x + min<int64_t>(r, N - 1) * F;
+      const double* hr = h1 + min<int64_t>(r, N - 1) * M;
+#pragma unroll
+      for (int h = 0; h < NH; ++h) xb[i][q][h] = xr[min(16 * h + fr, F - 1)];
+#pragma unroll
+      for (int j = 0; j < FC; ++j) hv[j][i][q] = hr[min(col0 + j * 16 + fr, M - 1)];
+    }
+#pragma unroll
+  for (int i = 0; i < FR; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const bool rin = row0 + wave * FR * 16 + i * 16 + 4 * q + g < N;
 #pragma unroll
       for (int h = 0; h < NH; ++h) {
+        // arithmetic, not a select: a select lets hipcc sink the load into a branch and wait
+        // for it there (the clamped x value is a finite state coordinate: x * 0 = 0)
         const int f = 16 * h + fr;
-        const double v = xr[min(f, F - 1)];
-        xb[i][q][h] = r < N ? (f < F ? v : (f == F ? 1.0 : 0.0)) : 0.0;
+        const double keep = (rin && f < F) ? 1.0 : 0.0, one = (rin && f == F) ? 1.0 : 0.0;
+        xb[i][q][h] = fma(xb[i][q][h], keep, one);
       }
     }
   double* red = lds;  // [WR][NH][4][64]: the main loop's last barrier retired its LDS reads
@@ -229,11 +249,7 @@ __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
     for (int i = 0; i < FR; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        // accumulator element (row g + 4 q of fragment i, col fr) is A[m = fr][k = g] of
-        // k-step (i, q): rows 16 i + 4 q + g
-        const int64_t r = row0 + wave * FR * 16 + i * 16 + g + 4 * q;
-        const double hv = h1[min<int64_t>(r, N - 1) * M + min(c, M - 1)];
-        const double dz = (hv > 0.0 && c < M) ? acc[i][j][q] : 0.0;
+        const double dz = (hv[j][i][q] > 0.0 && c < M) ? acc[i][j][q] : 0.0;
 #pragma unroll
         for (int h = 0; h < NH; ++h)
           dacc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(dz, xb[i][q][h], dacc[h], 0, 0, 0);

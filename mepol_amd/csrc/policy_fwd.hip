@@ -110,9 +110,7 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
       const int r = wave * 16 + g + 4 * q;
       const double v = c < H1 ? fmax(h[q] + bc, 0.0) : 0.0;
       sA[(buf * BM + r) * KP + fr] = v;
-#ifndef MEPOL_PF_NO_H1STORE
       if (c < H1 && row0 + r < N) h1_out[(row0 + r) * H1 + c] = v;
-#endif
     }
   };
 
@@ -219,9 +217,6 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
   double* sMu = sB;  // [WC][BM][kAChunk]; the loop's last barrier retired every sB read
   const int er = tid >> 3, ea = tid & 7;  // combine step: row er of the block, action slot ea
   double lp = 0.0;
-#ifdef MEPOL_PF_NO_HEAD
-  A = 0;
-#endif
   for (int a0 = 0; a0 < A; a0 += kAChunk) {
     double wmv[FC][kAChunk];
 #pragma unroll
