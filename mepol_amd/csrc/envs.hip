@@ -314,7 +314,8 @@ __global__ __launch_bounds__(64 * kRollMwWaves) void rollout_mlp_mw_kernel(
     const float* __restrict__ init32, const double* __restrict__ noise, int64_t n, int64_t T,
     float* __restrict__ states_rec, float* __restrict__ actions_rec,
     double* __restrict__ visited, double* __restrict__ final_state, int np, int nw,
-    unsigned long long* __restrict__ mail, int* __restrict__ err, long long* __restrict__ probe) {
+    unsigned long long* __restrict__ mail, int* __restrict__ err, int* __restrict__ ticket,
+    long long* __restrict__ probe) {
   extern __shared__ double sW2[];  // [h0][64]: W2^T rows, this part's 64 columns
   __shared__ double sh1[kRollMaxH];
   __shared__ double spart[kRollMwWaves][64];
@@ -331,8 +332,17 @@ __global__ __launch_bounds__(64 * kRollMwWaves) void rollout_mlp_mw_kernel(
       pt = now;
     }
   };
-  const int64_t i = blockIdx.x / np;
-  const int p = (int)(blockIdx.x % np);
+  // (trajectory, part) from a dispatch-order ticket, not from blockIdx: when a workgroup takes
+  // ticket t, every ticket below t is held by a running workgroup, so the parts a workgroup
+  // waits for are either running or next in line for a free slot.  With the whole grid
+  // resident (the host's occupancy check) all parts run at once; with fewer slots (another
+  // kernel on the CUs) complete trajectories still finish and free theirs: no deadlock without
+  // a cooperative launch.
+  __shared__ int sticket;
+  if (threadIdx.x == 0) sticket = atomicAdd(ticket, 1);
+  __syncthreads();
+  const int64_t i = sticket / np;
+  const int p = sticket % np;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int j = 64 * p + lane;
   const bool c1 = j < h1;
@@ -614,21 +624,22 @@ static int rollout_mw_prepare() {
   return 0;
 }
 
-// The multi-workgroup form needs every workgroup of a trajectory resident at once (its parts
-// exchange partial sums every step).  It is launched as a COOPERATIVE kernel, whose contract
-// is exactly that (all workgroups co-resident, or the launch fails), and only when the
-// occupancy of the kernel at this LDS size times the CU count holds the whole grid; otherwise
-// (and when the cooperative launch is refused) the one-workgroup form runs, which sums in the
-// same order and so gives the same bits.
+// The multi-workgroup form's parts exchange partial sums every step.  Its workgroups take
+// (trajectory, part) from a dispatch-order ticket (see the kernel), which makes the exchange
+// deadlock-free whenever a trajectory's np parts fit on the device; it is chosen only when the
+// occupancy of the kernel at this LDS size times the CU count holds the whole grid (all parts
+// in flight at once).  Otherwise the one-workgroup form runs, which sums in the same order and
+// so gives the same bits.  (Round 4 used hipLaunchCooperativeKernel for the co-residency; its
+// dedicated queue crashed the process at exit under rocprofv3: HIP's teardown of that queue
+// faulted inside libhsa-runtime64 after the profiler had shut its queue interception down,
+// profiles/r5/rollout_exit_crash.txt.)
 static int rollout_use_mw(int env_id, int64_t n, int h0, int h1, int a_dim) {
   const int np = (h1 + 63) / 64;
   const char* mw = getenv("MEPOL_ROLLOUT_MW");
   if (h0 > kRollMwMaxH0 || np * a_dim > 64 || (mw && mw[0] == '0')) return 0;
-  int dev = 0, cus = 0, coop = 0;
+  int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess ||
-      !coop)
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
     return 0;
   const size_t lds = (size_t)h0 * 64 * sizeof(double);
   int per_cu = 0;
@@ -683,17 +694,14 @@ static hipError_t rollout_mw_launch(const double* W1, const double* b1, int h0,
                                     const double* noise, int64_t n, int64_t T, float* states_rec,
                                     float* actions_rec, double* visited, double* final_state,
                                     int np, int nw, unsigned long long* mail, int* err,
-                                    hipStream_t st) {
+                                    int* ticket, hipStream_t st) {
   long long* probe = nullptr;
-  void* args[] = {(void*)&W1,         (void*)&b1,          (void*)&h0,      (void*)&W2t,
-                  (void*)&b2,         (void*)&h1,          (void*)&Wm,      (void*)&bm,
-                  (void*)&log_std,    (void*)&a_dim,       (void*)&init64,  (void*)&init32,
-                  (void*)&noise,      (void*)&n,           (void*)&T,       (void*)&states_rec,
-                  (void*)&actions_rec, (void*)&visited,    (void*)&final_state, (void*)&np,
-                  (void*)&nw,         (void*)&mail,        (void*)&err,     (void*)&probe};
-  return hipLaunchCooperativeKernel((const void*)rollout_mlp_mw_kernel<ENV>,
-                                    dim3((unsigned)(n * np)), dim3(64 * kRollMwWaves), args,
-                                    (unsigned)((size_t)h0 * 64 * sizeof(double)), st);
+  hipLaunchKernelGGL((rollout_mlp_mw_kernel<ENV>), dim3((unsigned)(n * np)),
+                     dim3(64 * kRollMwWaves), (unsigned)((size_t)h0 * 64 * sizeof(double)), st,
+                     W1, b1, h0, W2t, b2, h1, Wm, bm, log_std, a_dim, init64, init32, noise, n, T,
+                     states_rec, actions_rec, visited, final_state, np, nw, mail, err, ticket,
+                     probe);
+  return hipGetLastError();
 }
 
 extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1, int h0,
@@ -723,18 +731,20 @@ extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1,
     if (workspace && workspace_bytes >= rollout_mw_bytes(n, T, h1, a_dim) &&
         rollout_use_mw(env_id, n, h0, h1, a_dim)) {
       unsigned long long* mail = (unsigned long long*)((char*)workspace + 256);
+      int* ticket = err + 1;  // word 1 of the 256-byte header: the dispatch-order counter
+      MEPOL_HIP(hipMemsetAsync(ticket, 0, sizeof(int), st));
       // every mail word starts as kMailEmpty (all ones)
       MEPOL_HIP(hipMemsetAsync(mail, 0xff, (size_t)n * T * np * a_dim * 8, st));
       const hipError_t e =
           env_id == 0
               ? rollout_mw_launch<0>(W1, b1, h0, W2t, b2, h1, Wm, bm, log_std, a_dim, init64,
                                      init32, noise, n, T, states_rec, actions_rec, visited,
-                                     final_state, np, nw, mail, err, st)
+                                     final_state, np, nw, mail, err, ticket, st)
               : rollout_mw_launch<1>(W1, b1, h0, W2t, b2, h1, Wm, bm, log_std, a_dim, init64,
                                      init32, noise, n, T, states_rec, actions_rec, visited,
-                                     final_state, np, nw, mail, err, st);
+                                     final_state, np, nw, mail, err, ticket, st);
       if (e == hipSuccess) return 0;
-      (void)hipGetLastError();  // refused (e.g. hipErrorCooperativeLaunchTooLarge): one-wg form
+      (void)hipGetLastError();  // launch refused: the one-workgroup form
     }
   }
   const dim3 g((unsigned)n);
@@ -744,8 +754,6 @@ extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1,
   if (klv) KL = std::min(KL, atoi(klv));
   KL = std::max(0, std::min(KL, h0));
   const size_t lds = (size_t)KL * threads * sizeof(double);
-  const char* uv = getenv("MEPOL_ROLLOUT_U");
-  const int u = uv ? atoi(uv) : 8;
 #define MEPOL_ROLL(E, U)                                                                          \
   do {                                                                                            \
     static bool attr = false;                                                                     \
@@ -758,13 +766,10 @@ extern "C" int mepol_rollout_mlp(int env_id, const double* W1, const double* b1,
                        h1, Wm, bm, log_std, a_dim, init64, init32, noise, n, T, states_rec,       \
                        actions_rec, visited, final_state, KL);                                    \
   } while (0)
-  if (env_id == 0) {
-    if (u >= 16) MEPOL_ROLL(0, 16);
-    else MEPOL_ROLL(0, 8);
-  } else {
-    if (u >= 16) MEPOL_ROLL(1, 16);
-    else MEPOL_ROLL(1, 8);
-  }
+  if (env_id == 0)
+    MEPOL_ROLL(0, 8);
+  else
+    MEPOL_ROLL(1, 8);
 #undef MEPOL_ROLL
   MEPOL_CHECK_LAUNCH();
   return 0;

@@ -64,6 +64,8 @@ def _run(monkeypatch, graph, opt_name, lr, kl_threshold, max_off_iters=6, cfg=No
         backtracking, 2, 4, lr,
         on_accept=lambda n, e, kl, l: trace.append((n, float(e), float(kl), l)))
     used = tgt in device_loop._CACHE
+    it = device_loop._CACHE.get(tgt)
+    fused = (it.fused_fwd, it.fused_dh1) if it is not None else None
     params = torch.cat([p.detach().reshape(-1) for p in last.parameters()]).cpu().numpy()
     state = opt.state_dict()["state"]
     steps = [float(state[i]["step"]) for i in sorted(state)]
@@ -72,7 +74,8 @@ def _run(monkeypatch, graph, opt_name, lr, kl_threshold, max_off_iters=6, cfg=No
                               if key != "step"])
     tparams = torch.cat([p.detach().reshape(-1) for p in tgt.parameters()]).cpu().numpy()
     return dict(H=float(res[0]), n=res[1], bt=res[2], lr=res[3], trace=trace, params=params,
-                steps=steps, used=used, raw=raw, D=D, I=I, moments=moments, tparams=tparams)
+                steps=steps, used=used, raw=raw, D=D, I=I, moments=moments, tparams=tparams,
+                fused=fused)
 
 
 def _assert_same_run(g, e):
@@ -263,3 +266,19 @@ def test_graph_loop_fresh_batch_after_rejection(cuda, monkeypatch):
             np.testing.assert_allclose(a[1:], b[1:], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(g_params, e_params, rtol=1e-8, atol=1e-11)
     np.testing.assert_allclose(g_mom, e_mom, rtol=1e-8, atol=1e-14)
+
+
+@pytest.mark.parametrize("fwd,dh1", [("0", "1"), ("1", "0"), ("0", "0")])
+def test_unfused_mlp_kernels_match_fused(cuda, monkeypatch, fwd, dh1):
+    """MEPOL_FUSED_FWD=0 / MEPOL_FUSED_DH1=0 select the unfused forward (layer kernels + GEMM)
+    and backward (dh1 GEMM + separate layer-1 backward) inside the captured iteration, the form
+    used where the fused kernels' shape limits are not met; both forms agree with each other."""
+    ref = _run(monkeypatch, True, "adam", 1e-4, 1e9, max_off_iters=3, cfg=C3)
+    monkeypatch.setenv("MEPOL_FUSED_FWD", fwd)
+    monkeypatch.setenv("MEPOL_FUSED_DH1", dh1)
+    got = _run(monkeypatch, True, "adam", 1e-4, 1e9, max_off_iters=3, cfg=C3)
+    assert got["used"] and ref["used"] and got["n"] == ref["n"] == 3
+    assert ref["fused"] == (True, True) and got["fused"] == (fwd == "1", dh1 == "1")
+    for a, b in zip(got["trace"], ref["trace"]):
+        np.testing.assert_allclose(a[1:3], b[1:3], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(got["params"], ref["params"], rtol=1e-8, atol=1e-11)

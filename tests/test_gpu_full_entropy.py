@@ -19,9 +19,14 @@ from oracle import mepol_oracle as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("num_traj,scale,traj_len,fe_k", [(4, 2, 400, 4), (2, 5, 250, 4),
-                                                          (3, 2, 300, 7)])
-def test_full_entropy_batch_matches_oracle(cuda, num_traj, scale, traj_len, fe_k):
+# GridWorld rollouts revisit states exactly (blocked moves at the walls), so with eps = 0 a
+# duplicate-heavy batch gives d_k = 0 and H = -inf, in the reference as here; eps = 1e-15 (the
+# experiments' value for MountainCar, experiments/mepol.py) keeps it finite.
+@pytest.mark.parametrize("num_traj,scale,traj_len,fe_k,eps", [(4, 2, 400, 4, 1e-15),
+                                                              (2, 5, 250, 4, 1e-15),
+                                                              (3, 2, 300, 7, 1e-15),
+                                                              (4, 2, 400, 4, 0.0)])
+def test_full_entropy_batch_matches_oracle(cuda, num_traj, scale, traj_len, fe_k, eps):
     from mepol_amd.algorithms import mepol as M
     from mepol_amd.envs import ErgodicEnv, GridWorldContinuous
     from mepol_amd.policy import GaussianPolicy
@@ -36,7 +41,6 @@ def test_full_entropy_batch_matches_oracle(cuda, num_traj, scale, traj_len, fe_k
     ns = env.num_features
     G = scipy.special.gamma(ns / 2 + 1)
     full_B = np.log(fe_k) - scipy.special.digamma(fe_k)
-    eps = 0.0
     with torch.no_grad():
         H = M.compute_entropy(pol, pol, st, ac, nt, rl, D, I, fe_k, G, full_B, ns, eps)
     assert H.device.type == "cpu" and H.dtype == torch.float64 and H.dim() == 0
@@ -52,8 +56,10 @@ def test_full_entropy_batch_matches_oracle(cuda, num_traj, scale, traj_len, fe_k
     w = O.importance_weights(lp, lp, [traj_len] * nt)
     np.testing.assert_array_equal(w, np.full(nt * traj_len, 1.0 / (nt * traj_len)))
     H_ref = O.entropy(w, Do, Io, fe_k, G, full_B, ns, eps)
-    assert np.isfinite(H_ref)
-    np.testing.assert_allclose(float(H), H_ref, rtol=1e-9)
+    if not np.isfinite(H_ref):
+        assert eps == 0.0 and float(H) == H_ref  # -inf on both sides
+    else:
+        np.testing.assert_allclose(float(H), H_ref, rtol=1e-9)
 
 
 @pytest.mark.parametrize("name", ["policy_gw", "policy_ant", "policy_pretrained_gw"])

@@ -4,10 +4,10 @@ set -o pipefail
 out=gpurun_out/${1:-segv}
 mkdir -p "$out"
 root=$(pwd)
-timeout -k 10 400 python -u -m pytest tests/test_gpu_full_entropy.py tests/test_gpu_entropy.py -x -v --timeout 200 --timeout-method thread > "$out/tests.log" 2>&1 || { tail -40 "$out/tests.log"; exit 1; }
+[ -n "$SKIP_TESTS" ] || timeout -k 10 400 python -u -m pytest tests/test_gpu_full_entropy.py tests/test_gpu_entropy.py tests/test_gpu_envs.py "tests/test_gpu_device_loop.py::test_unfused_mlp_kernels_match_fused" -x -v --timeout 200 --timeout-method thread > "$out/tests.log" 2>&1 || { tail -40 "$out/tests.log"; exit 1; }
 tail -3 "$out/tests.log"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$root/$out/prof" -o run -- python3 "$root/tools/segv_run.py" "$root/bench.py" --workload C2S --steps 2 --no-cpu-baseline > "$root/$out/c2s.json" 2> "$root/$out/c2s.err"
+SEGV_RUN_MAPS="$root/$out/maps.txt" timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$root/$out/prof" -o run -- python3 "$root/tools/segv_run.py" "$root/bench.py" --workload C2S --steps 2 --no-cpu-baseline > "$root/$out/c2s.json" 2> "$root/$out/c2s.err"
 rc=$?
 echo "rocprofv3 C2S rc=$rc"
 tail -60 "$root/$out/c2s.err"

@@ -33,7 +33,7 @@ def main(n=20, T=1000, h0=300, h1=300, reps=5):
     st = torch.empty((n, T + 1, 2), dtype=torch.float32, device=dev)
     ac = torch.empty((n, T, 2), dtype=torch.float32, device=dev)
     mail = torch.empty(n * T * np_ * 2, dtype=torch.int64, device=dev)
-    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    err = torch.zeros(2, dtype=torch.int32, device=dev)  # [error flag, dispatch ticket]
     probe = torch.zeros((n * np_, 8), dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream()
     P = lambda t: ctypes.c_void_p(t.data_ptr())
@@ -49,7 +49,7 @@ def main(n=20, T=1000, h0=300, h1=300, reps=5):
             ctypes.c_void_p(s.cuda_stream))
         e1.record()
         torch.cuda.synchronize()
-        assert rc == 0 and int(err.item()) == 0, (rc, int(err.item()))
+        assert rc == 0 and int(err[0].item()) == 0, (rc, int(err[0].item()))
         res.append((e0.elapsed_time(e1), probe.cpu().numpy().copy()))
     ms, pr = res[-1]
     cyc = pr[:, :5].sum(1).astype(np.float64)

@@ -31,6 +31,6 @@ extern "C" int probe_rollout_mw_gridworld(const double* W1, const double* b1, in
   hipLaunchKernelGGL((rollout_mlp_mw_kernel<1, true>), dim3((unsigned)(n * np)), dim3(64 * kRollMwWaves),
                      (size_t)h0 * 64 * 8, (hipStream_t)stream, W1, b1, h0, W2t, b2, h1, Wm, bm,
                      log_std, 2, nullptr, init32, noise, n, T, states_rec, actions_rec, nullptr,
-                     nullptr, np, nw, mail, err, probe);
+                     nullptr, np, nw, mail, err, err + 1, probe);  // err[1]: ticket (zeroed)
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
