@@ -79,6 +79,9 @@ def parse(argv=None):
     p.add_argument("--workload", default="C3", choices=sorted(WORKLOADS))
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample-queries", type=int, default=16000)
+    p.add_argument("--no-pmc", action="store_true",
+                   help="skip the live rocprofv3 --pmc passes for roofline.traffic (the stamped "
+                        "profiles/knn_pmc_<workload>.json is read instead)")
     p.add_argument("--selftest", action="store_true",
                    help="launcher plumbing only (no GPU): ranks rendezvous over gloo, time an "
                         "empty step with the max-over-ranks clock and print the JSON line")
@@ -413,9 +416,13 @@ def run(args):
     knn_desc = (("f16 MFMA selection (candidate hi half x split query" if plan["nh"] == 1 else
                  "f16 MFMA selection (split candidate x split query, 3 products")
                 + ", f32 accumulate) + certified f64 exact refine (bit-exact output)")
-    traffic, traffic_note = None, None
+    traffic, traffic_note, traffic_kernels = None, None, None
+    live = getattr(args, "live_traffic", None)
     pmc_path = os.path.join(ROOT, "profiles", f"knn_pmc_{args.workload}.json")
-    if os.path.exists(pmc_path) and world == 1:  # counters were taken on the 1-GPU k-NN call
+    if live is not None and live[0] is not None:
+        traffic, traffic_kernels = live[0], live[1]
+    elif os.path.exists(pmc_path) and world == 1 and emul is None:
+        # counters were taken on the 1-GPU k-NN call
         # the PMC passes (tools/knn_pmc.sh -> tools/knn_pmc_summary.py) stamp the file with a
         # hash of the k-NN sources they measured; a file from other sources is not reported
         try:
@@ -464,9 +471,20 @@ def run(args):
                                 "call + index all-gather + CSR build), HIP events")
                                + "; achieved = F/t, F = 3*d*Nq*Nc (SURVEY 8d)"},
     }
+    if live is not None and live[0] is None:
+        traffic_note = f"live PMC passes failed ({live[2]})" + (
+            f"; {traffic_note}" if traffic_note else
+            (f"; reported from {os.path.relpath(pmc_path, ROOT)}" if traffic else ""))
     if traffic_note:
         line["roofline"]["traffic_note"] = traffic_note
-    if traffic:
+    if traffic and traffic_kernels is not None:
+        line["roofline"]["traffic_source"] = (
+            "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (one counter each) over "
+            "tools/knn_probe.py at this shape, run by this bench before it touched the GPU; "
+            "FETCH_SIZE x2 (gfx950)")
+        line["roofline"]["traffic_per_kernel"] = traffic_kernels
+        line["roofline"]["traffic_compulsory"] = 4 * d * (nq + N) + 8 * (k + 1) * nq
+    elif traffic:
         line["roofline"]["traffic_source"] = os.path.relpath(pmc_path, ROOT)
         gbps = traffic / (knn_ms * 1e-3) / 1e9
         line["roofline"]["hbm_GBps"] = round(gbps, 1)
@@ -661,11 +679,71 @@ def cpu_baseline(cfg, sample_queries, iters_done):
             "calibration_vs_reference": ratio}
 
 
+def _under_profiler():
+    return ("rocprof" in os.environ.get("LD_PRELOAD", "")
+            or any(k.startswith("ROCPROF") for k in os.environ))
+
+
+def live_knn_traffic(cfg):
+    """HBM bytes of one k-NN call at this workload's shape, measured in THIS bench run: two
+    rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE: one counter per pass, as MI355X_MICROARCH.md
+    prescribes) over tools/knn_probe.py as child processes, started before this process touches
+    the GPU.  FETCH_SIZE is doubled (gfx950), WRITE_SIZE taken as reported (tools/knn_pmc_summary).
+    Returns (bytes, per-kernel dict, note) or (None, None, reason)."""
+    import shutil
+    import signal
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, None, "rocprofv3 not on PATH"
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from knn_pmc_summary import per_call
+
+    N, d, k = cfg["num_traj"] * cfg["traj_len"], cfg["d"], cfg["k"]
+    out = tempfile.mkdtemp(prefix="mepol_pmc_", dir="/tmp")
+    res = {}
+    for c in ("FETCH_SIZE", "WRITE_SIZE"):
+        cmd = [prof, "--pmc", c, "-d", os.path.join(out, c), "-o", "run", "--", sys.executable,
+               os.path.join(ROOT, "tools", "knn_probe.py"), "--n", str(N), "--d", str(d),
+               "--kp1", str(k + 1), "--reps", "1"]
+        p = subprocess.Popen(cmd, cwd="/tmp", env=dict(os.environ, TMPDIR="/tmp"),
+                             stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                             start_new_session=True)
+        try:
+            rc = p.wait(timeout=150)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            return None, None, f"rocprofv3 --pmc {c} pass timed out"
+        if rc != 0:
+            return None, None, f"rocprofv3 --pmc {c} pass exited {rc}"
+        try:
+            res[c] = per_call(os.path.join(out, c, "run_results.db"), c)
+        except Exception as e:  # no database / no k-NN dispatch in it
+            return None, None, f"rocprofv3 --pmc {c} output unreadable: {e!r}"
+    shutil.rmtree(out, ignore_errors=True)
+    fetch, write = res["FETCH_SIZE"], res["WRITE_SIZE"]
+    kernels = {kk.split("::")[-1][:60]: {"fetch_x2": round(2 * fetch.get(kk, 0.0)),
+                                          "write": round(write.get(kk, 0.0))}
+               for kk in sorted(set(fetch) | set(write))}
+    total = sum(2 * v for v in fetch.values()) + sum(write.values())
+    return total, kernels, None
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return spawn(args, argv)
+    cfg = WORKLOADS[args.workload]
+    args.live_traffic = None
+    if (not args.no_pmc and not args.selftest and "WORLD_SIZE" not in os.environ
+            and cfg.get("env") is None and not cfg.get("emulate_world")):
+        if _under_profiler():
+            args.live_traffic = (None, None, "bench runs under a profiler: live PMC passes skipped")
+        else:  # before this process makes any GPU call
+            args.live_traffic = live_knn_traffic(cfg)
     run(args)
     return 0
 

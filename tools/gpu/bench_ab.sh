@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4: bench lines under env A/B settings: tools/r4_bench_ab.sh outdir workload VAR=a VAR=b
+# bench lines under env A/B settings: tools/gpu/bench_ab.sh outdir workload VAR=a VAR=b
 set -o pipefail
 out=gpurun_out/${1:-r4bab}; w=$2; shift 2
 mkdir -p "$out"

@@ -1,9 +1,9 @@
 #!/bin/bash
-# round 4 final: full GPU suite, smoke, k-NN HBM counters (stamped), the default bench line, the
+# final checkpoint: full GPU suite, smoke, k-NN HBM counters (stamped), the default bench line, the
 # same bench command under rocprofv3 --kernel-trace --stats, and the C3R8 line.  Stops at the
 # first failing step.
 set -o pipefail
-out=gpurun_out/${1:-r4final}
+out=gpurun_out/${1:-final}
 mkdir -p "$out"
 echo "[final] gpu tests"
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
@@ -20,7 +20,7 @@ timeout -k 10 400 python -u bench.py > "$out/bench_default.json" 2> "$out/bench_
 cat "$out/bench_default.json"
 echo "[final] bench under rocprofv3"
 root=$(pwd)
-( cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$root/$out/prof" -o run -- python3 "$root/bench.py" > "$root/$out/bench_prof.json" 2> "$root/$out/bench_prof.err" ) || { tail -20 "$out/bench_prof.err"; exit 1; }
+( cd /tmp && export TMPDIR=/tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$root/$out/prof" -o run -- python3 "$root/bench.py" --no-pmc > "$root/$out/bench_prof.json" 2> "$root/$out/bench_prof.err" ) || { tail -20 "$out/bench_prof.err"; exit 1; }
 cat "$out/bench_prof.json"
 echo "[final] bench C3R8"
 timeout -k 10 300 python -u bench.py --workload C3R8 --no-cpu-baseline > "$out/bench_C3R8.json" 2> "$out/bench_C3R8.err" || { tail -20 "$out/bench_C3R8.err"; exit 1; }

@@ -1,6 +1,6 @@
 #!/bin/bash
-# round 4: bench lines + kernel traces -> one off-policy iteration's timeline
-# usage: tools/r4_timeline.sh outdir workload [ENV=VAL ...]
+# bench lines + kernel traces -> one off-policy iteration's timeline
+# usage: tools/gpu/timeline.sh outdir workload [ENV=VAL ...]
 set -o pipefail
 root=$GRAFT_REPO_ROOT
 out=$root/gpurun_out/${1:-r4t}
