@@ -139,7 +139,7 @@ class _EmulatedDist:
     all_gather_into_tensor fills the peers' slots from `peers` (a list of world - 1 tensors)
     when one of that shape and dtype is registered -- the other shards' next states, so the
     k-NN runs against the full candidate set -- and with rank 0's own payload otherwise;
-    all_reduce keeps rank 0's values.  Per-rank compute of the multi-GPU run, not its result."""
+    all_reduce keeps rank 0's values (one in-place pass over the payload).  Per-rank compute of the multi-GPU run, not its result."""
 
     class ReduceOp:
         SUM, MIN, MAX = "sum", "min", "max"
@@ -170,7 +170,10 @@ class _EmulatedDist:
             o[r].copy_(pe[r - 1].reshape(-1))
 
     def all_reduce(self, t, op=None, group=None):
-        return None
+        # a device pass over the same payload in place (x * 1 is exact): one launch that reads
+        # and writes the bytes, a lower bound for RCCL's reduce-scatter + all-gather (the xGMI
+        # cost model is DESIGN.md section 6)
+        t.mul_(1.0)
 
 
 def selftest(args):

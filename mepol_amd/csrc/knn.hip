@@ -512,7 +512,7 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   if (d > kScreenMaxD || kp1 > kScreenMaxKp1) return make_exhaustive_plan(P);
   P->KS16 = (d + 1 + 15) / 16;
   // f16 lists: each half-lane keeps LIST16 entries and prunes against the union bound
-  // (flush_buffer, keep = ceil(kp1/2) + 2 per half: 2 keep >= kp1 + 3).  A half holding more
+  // (flush_groups, keep = ceil(kp1/2) + 2 per half: 2 keep >= kp1 + 3).  A half holding more
   // than LIST16 of the query's nearest candidates only costs certification (exact path).
   P->keep = (kp1 + 1) / 2 + 2;
   P->LIST16 = 40;

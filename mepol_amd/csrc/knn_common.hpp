@@ -18,10 +18,6 @@ using f32x4 = __attribute__((ext_vector_type(4))) float;
 using f16x8 = __attribute__((ext_vector_type(8))) _Float16;
 
 
-#ifndef MEPOL_BUFCAP
-#define MEPOL_BUFCAP 20
-#endif
-constexpr int kBufCap = MEPOL_BUFCAP;  // per-lane LDS insertion buffer (entries)
 constexpr int kMaxSplit = 16;
 constexpr int kExactGrid = 512;    // blocks of the exhaustive fallback (exact_kernel)
 constexpr int kRefineList = 64;    // approximate candidates refine ranks per query (one wave)
@@ -44,47 +40,12 @@ __device__ __forceinline__ void list_insert(float (&ld)[LIST], int (&li)[LIST], 
   li[0] = c[0] ? xi : li[0];
 }
 
-// Merge this lane's LDS buffer into its sorted list; then share the prune bound with the
-// partner lane (l ^ 32 serves the same query column).  Every lane of the wave calls it.
-// keep > 0 (split-f16 select): the bound also takes max(own keep-th, partner's keep-th): the
-// two half lists then hold >= 2 keep values at or below it, so 2 keep >= kp1 + slack of the
-// query's candidates in this range are never pruned; this bound is far tighter than a list's
-// own last entry (the LIST-th of one half).  The bound only decreases over the scan.
 template <int LIST>
 __device__ __forceinline__ float list_at(const float (&ld)[LIST], int j) {
   float v = INFINITY;
 #pragma unroll
   for (int i = 0; i < LIST; ++i) v = (i == j) ? ld[i] : v;
   return v;
-}
-
-template <int LIST>
-__device__ __forceinline__ void flush_buffer(float (&ld)[LIST], int (&li)[LIST], float& thr, int& cnt,
-                                             const float2 (*buf)[64], int l, float thr0,
-                                             int keep = 0) {
-  const int mc = wave_max_i(cnt);
-  // entry e + 1 is read from LDS while entry e is inserted (the read latency would otherwise
-  // sit in front of every insertion)
-  float2 cur = buf[0][l];
-#pragma nounroll
-  for (int e = 0; e < mc; ++e) {
-    const int en = min(e + 1, kBufCap - 1);
-    const float2 nxt = buf[en][l];
-    if (e < cnt && cur.x < thr) {
-      list_insert<LIST>(ld, li, cur.x, __float_as_int(cur.y));
-      thr = ld[LIST - 1];
-    }
-    cur = nxt;
-  }
-  cnt = 0;
-  // lanes l and l^32 serve the same query: the tighter of their maxima is a valid prune bound
-  // for both (refine's certification bound is the min over all lanes' final bounds and the
-  // query's sampled bound thr0).
-  thr = fminf(thr0, fminf(ld[LIST - 1], __shfl_xor(ld[LIST - 1], 32, kWave)));
-  if (keep > 0) {
-    const float kv = list_at<LIST>(ld, keep - 1);
-    thr = fminf(thr, fmaxf(kv, __shfl_xor(kv, 32, kWave)));
-  }
 }
 
 // LDS byte address of a __shared__ object (the M0 operand of an LDS-DMA load); wave-uniform.
