@@ -170,10 +170,10 @@ class _EmulatedDist:
             o[r].copy_(pe[r - 1].reshape(-1))
 
     def all_reduce(self, t, op=None, group=None):
-        # a device pass over the same payload in place (x * 1 is exact): one launch that reads
+        # a device pass over the same payload in place (x * 1 is exact, any dtype): one launch that reads
         # and writes the bytes, a lower bound for RCCL's reduce-scatter + all-gather (the xGMI
         # cost model is DESIGN.md section 6)
-        t.mul_(1.0)
+        t.mul_(1)
 
 
 def selftest(args):

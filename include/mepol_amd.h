@@ -227,6 +227,16 @@ int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double*
                               double* db1, void* workspace, size_t workspace_bytes,
                               void* stream);
 
+/* Weight gradient of a linear layer over a tall batch: dW [out, in] = dy^T x with dy [n, out]
+ * and x [n, in] row-major f64 (the policy's dW2 = dz2^T h1, K = n), split-K on the f64 matrix
+ * cores and summed over the K-slices in a fixed order; workspace from
+ * mepol_weight_grad_workspace_size.  Replaces the weight gradient of the second Linear in
+ * loss.backward() (src/policy.py:21-26, mepol.py:278). */
+int mepol_weight_grad_workspace_size(int64_t n, int out_features, int in_features, size_t* bytes);
+int mepol_weight_grad(const double* dy, int64_t n, int out_features, const double* x,
+                      int in_features, double* dW, void* workspace, size_t workspace_bytes,
+                      void* stream);
+
 /* Hidden layer on the f64 matrix cores: C = act(A B^T + bias), A [n, k] (row stride lda),
  * B [m, k] (ldb), bias [m] (nullable), C [n, m] (ldc); act = ReLU when relu != 0.  k, lda, ldb
  * even and A, B 16-byte aligned.  variant 0 = default tiling.  Replaces the torch.mm /

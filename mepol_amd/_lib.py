@@ -52,6 +52,8 @@ SIGNATURES = {
     "mepol_head_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
     "mepol_head_backward": [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int,
                             _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
+    "mepol_weight_grad_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
+    "mepol_weight_grad": [_c_vp, _c_i64, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_layer_forward": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp],
     "mepol_layer_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
     "mepol_layer_backward": [_c_vp, _c_vp, _c_vp, _c_i64, _c_int, _c_int, _c_vp, _c_vp, _c_vp, _c_sz,

@@ -30,7 +30,7 @@ import torch
 import torch.nn as nn
 
 from .. import ops
-from ..policy import GaussianPolicy, _weight_grad
+from ..policy import GaussianPolicy
 
 _ADAM, _RMSPROP = 0, 1
 
@@ -148,6 +148,7 @@ class DeviceIteration:
         self.ws_head = ops.head_workspace(self.N, W2.shape[0], Wm.shape[0], dev)
         self.ws_layer = ops.layer_workspace(self.N, W1.shape[1], W1.shape[0], dev)
         self.ws_dh1 = ops.dh1_layer1_workspace(self.N, W1.shape[0], W1.shape[1], dev)
+        self.ws_wgrad = ops.weight_grad_workspace(self.N, W2.shape[0], W2.shape[1], dev)
         self.graph = None
         self.fork = torch.cuda.Stream(device=dev)
         self.s_gemm = torch.cuda.Stream(device=dev)
@@ -289,7 +290,7 @@ class DeviceIteration:
         are written, concurrent with the dh1 / layer-1 backward (the sharded iteration starts
         that bucket's all-reduce there).
 
-        Head backward, then dW2 (split-K GEMM, forked stream) concurrent with the fused
+        Head backward, then dW2 (split-K f64 MFMA, csrc/wgrad.hip, forked stream) concurrent with the fused
         dh1 -> layer-1 backward (measured: faster than dh1 first with dW2 overlapping the
         layer-1 backward, and than splitting dW2 across both phases)."""
         W1, b1, W2, b2, Wm, bm, ls = self.named
@@ -310,7 +311,7 @@ class DeviceIteration:
         e_h.record(cur)
         self.fork.wait_event(e_h)
         with torch.cuda.stream(self.fork):
-            dW2 = _weight_grad(dz2, self.h1, out=o[2])
+            dW2 = ops.weight_grad(dz2, self.h1, out=o[2], ws=self.ws_wgrad)  # csrc/wgrad.hip
             if after_dW2 is not None:
                 after_dW2()
         self.s_gemm.wait_event(e_h)

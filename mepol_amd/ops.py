@@ -422,6 +422,31 @@ def dh1_layer1_backward(dz2, W2t, h1, x, ws=None, dW_out=None, db_out=None):
     return dW, db
 
 
+def weight_grad_workspace(n, out_features, in_features, device):
+    """Scratch of weight_grad (its K-slices' partial blocks), owned by the caller."""
+    import ctypes
+
+    nbytes = ctypes.c_size_t()
+    call("mepol_weight_grad_workspace_size", n, out_features, in_features, ctypes.byref(nbytes))
+    return torch.empty(max(nbytes.value, 1), dtype=torch.uint8, device=device)
+
+
+def weight_grad(dy, x, out=None, ws=None):
+    """dW = dy^T x for dy [n, out] and x [n, in] (f64, row-major): the weight gradient of a
+    Linear layer over a tall batch (csrc/wgrad.hip: split-K on the f64 matrix cores, fixed-order
+    sum over the K-slices)."""
+    n, o = dy.shape
+    i = x.shape[1]
+    assert x.shape[0] == n and dy.is_contiguous() and x.is_contiguous()
+    assert dy.dtype == torch.float64 and x.dtype == torch.float64
+    if ws is None:
+        ws = weight_grad_workspace(n, o, i, dy.device)
+    dW = out if out is not None else torch.empty((o, i), dtype=torch.float64, device=dy.device)
+    assert dW.is_contiguous() and dW.shape == (o, i)
+    call("mepol_weight_grad", ptr(dy), n, o, ptr(x), i, ptr(dW), ptr(ws), ws.numel(), _stream())
+    return dW
+
+
 def gemm_nt(A, B, bias=None, relu=False, out=None, variant=0):
     """act(A B^T + bias) on the f64 matrix cores: A [n, k], B [m, k] (row-major, k even)."""
     n, k = A.shape

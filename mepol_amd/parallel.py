@@ -169,9 +169,13 @@ class ShardedEpoch:
         return H, KL, g
 
     # -- drop-in equivalents of the module-level functions ------------------------------------
-    def compute_entropy(self, beh, tgt, k, G, B, ns, eps):
+    def _entropy(self, beh, tgt, k, G, B, ns, eps):
         lt, lb = self._logps(beh, tgt)
         return _ShardedEntropy.apply(lt, lb, self, k, G, B, ns, eps)
+
+    def compute_entropy(self, beh, tgt, k, G, B, ns, eps):
+        """H on the host, as the module-level compute_entropy returns it (mepol.py:367-368)."""
+        return self._entropy(beh, tgt, k, G, B, ns, eps).cpu()
 
     def compute_kl_deferred(self, beh, tgt, k, eps):
         from .algorithms.particles import _param_key
@@ -193,7 +197,7 @@ class ShardedEpoch:
 
     def compute_kl(self, beh, tgt, k, eps):
         kl, flag = self.compute_kl_deferred(beh, tgt, k, eps)
-        return kl, bool(flag)
+        return kl.cpu(), bool(flag)  # host tensor, as the module-level compute_kl
 
     def allreduce_grads(self, params):
         grads = [p.grad for p in params if p.grad is not None]
@@ -209,7 +213,7 @@ class ShardedEpoch:
 
     def policy_update_deferred(self, optimizer, beh, tgt, k, G, B, ns, eps):
         optimizer.zero_grad()
-        loss = -self.compute_entropy(beh, tgt, k, G, B, ns, eps)
+        loss = -self._entropy(beh, tgt, k, G, B, ns, eps)
         flag = ~torch.isfinite(loss.detach())
         loss.backward()
         self.allreduce_grads(list(tgt.parameters()))
@@ -218,7 +222,7 @@ class ShardedEpoch:
 
     def policy_update(self, optimizer, beh, tgt, k, G, B, ns, eps):
         loss, flag = self.policy_update_deferred(optimizer, beh, tgt, k, G, B, ns, eps)
-        return loss, bool(flag)
+        return loss.detach().cpu(), bool(flag)  # host tensor, as the module-level policy_update
 
     def off_policy_optimization(self, optimizer, beh, tgt, last_valid, G, B, ns, eps,
                                 kl_threshold, max_off_iters, use_backtracking, backtrack_coeff,

@@ -32,11 +32,16 @@ def _split_count(n):
 
 
 def _weight_grad(gy, x, out=None):
-    """gy^T x for a tall batch as a split-K batched GEMM (into `out` when given).
-
-    A plain mm with K = N (200k) runs at 0.1-4.5 TFLOP/s in f64 on rocBLAS; 32 K-slices as one
-    bmm plus a reduction run at the shape's GEMM rate (tools/gemm_probe.py)."""
+    """gy^T x for a tall batch (into `out` when given): f64 on the GPU runs the split-K kernel
+    of csrc/wgrad.hip; otherwise a split-K batched GEMM (a plain mm with K = N = 200k runs at
+    0.1-4.5 TFLOP/s in f64 on rocBLAS; K-slices as one bmm plus a reduction run at the shape's
+    GEMM rate, tools/gemm_probe.py)."""
     n = gy.shape[0]
+    if (gy.is_cuda and gy.dtype == torch.float64 and x.dtype == torch.float64
+            and gy.is_contiguous() and x.is_contiguous() and n >= SPLITK_MIN_ROWS):
+        from . import ops  # split-K on the f64 matrix cores (csrc/wgrad.hip)
+
+        return ops.weight_grad(gy, x, out=out)
     if n < SPLITK_MIN_ROWS:
         return torch.mm(gy.t(), x, out=out) if out is not None else gy.t() @ x
     sk = _split_count(n)
