@@ -267,11 +267,15 @@ static void launch_select16_ks(const SelectArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((select16_kernel<KS16, L, NH, O>), g, dim3(256), 0, st, a.apack, a.query,  \
                      a.nq, a.d, a.nct, a.split, a.tiles_per_split, a.keep, a.scal, a.out_v,      \
                      a.out_i, a.seed)
+#ifndef MEPOL_SEL_OCC_KS3
+#define MEPOL_SEL_OCC_KS3 3
+#endif
+  constexpr int O3 = KS16 >= 3 ? MEPOL_SEL_OCC_KS3 : 3;
   switch (a.LIST16) {  // >= keep + 4 >= 7; split-candidate plans keep the instances that fit
     case 8: MEPOL_SEL16(8, 3); break;
-    case 16: MEPOL_SEL16(16, 3); break;
-    case 22: MEPOL_SEL16(22, 3); break;
-    case 24: MEPOL_SEL16(24, 3); break;
+    case 16: MEPOL_SEL16(16, O3); break;
+    case 22: MEPOL_SEL16(22, O3); break;
+    case 24: MEPOL_SEL16(24, O3); break;
     case 32: MEPOL_SEL16(32, 1); break;
     default:
       if constexpr (NH == 1 || KS16 <= 2) MEPOL_SEL16(40, 1);
