@@ -267,10 +267,9 @@ static void launch_select16_ks(const SelectArgs& a, hipStream_t st) {
   hipLaunchKernelGGL((select16_kernel<KS16, L, NH, O>), g, dim3(256), 0, st, a.apack, a.query,  \
                      a.nq, a.d, a.nct, a.split, a.tiles_per_split, a.keep, a.scal, a.out_v,      \
                      a.out_i, a.seed)
-#ifndef MEPOL_SEL_OCC_KS3
-#define MEPOL_SEL_OCC_KS3 3
-#endif
-  constexpr int O3 = KS16 >= 3 ? MEPOL_SEL_OCC_KS3 : 3;
+  // 3 waves per SIMD also for 3-4 k-steps, despite a few spilled dwords there: 2 waves per
+  // SIMD measured slower at d = 47 (6.14 -> 6.57 ms select; profiles/r5/knn/occ_ks3_ab.txt)
+  constexpr int O3 = 3;
   switch (a.LIST16) {  // >= keep + 4 >= 7; split-candidate plans keep the instances that fit
     case 8: MEPOL_SEL16(8, 3); break;
     case 16: MEPOL_SEL16(16, O3); break;

@@ -1,4 +1,4 @@
-"""One launch each of the fused forward and the fused dh1 + layer-1 backward at the C3 shapes
+"""One launch each of the fused forward, the fused dh1 + layer-1 backward and the dW2 kernel at the C3 shapes
 (for PMC passes: rocprofv3 --pmc ... -- python tools/mlp_kernels_once.py)."""
 import os
 import sys
@@ -22,8 +22,10 @@ h1, z2, mu, lp = ops.policy_forward(x, W1, b1, W2, b2, Wm, bm, ls, act)
 dz2 = torch.randn(N, H1, **f64)
 W2t = W2.t().contiguous()
 ws = ops.dh1_layer1_workspace(N, H0, F, dev)
+wsg = ops.weight_grad_workspace(N, H1, H0, dev)
 for _ in range(2):
     ops.policy_forward(x, W1, b1, W2, b2, Wm, bm, ls, act, h1, z2, mu, lp)
     ops.dh1_layer1_backward(dz2, W2t, h1, x, ws=ws)
+    ops.weight_grad(dz2, h1, ws=wsg)
 torch.cuda.synchronize()
 print("done")
