@@ -556,8 +556,10 @@ def _mlp_roofline(it):
 
     with torch.no_grad():
         t_f = timed(lambda: ops.policy_forward(it.x, W1, b1, W2, b2, Wm, bm, ls, it.act, it.h1,
-                                               it.z2, it.mu, it.logp))
-        t_b = timed(lambda: ops.dh1_layer1_backward(dz2, W2t, it.h1, it.x, ws=it.ws_dh1))
+                                               it.z2, it.mu, it.logp,
+                                               mask_out=getattr(it, "h1_mask", None)))
+        t_b = timed(lambda: ops.dh1_layer1_backward(dz2, W2t, it.h1, it.x, ws=it.ws_dh1,
+                                                    mask=getattr(it, "h1_mask", None)))
     fl_f = 2.0 * N * (h0 * h1w + F * h0)
     fl_b = 2.0 * N * (h1w * h0 + h0 * (F + 1))
     out = {"bound": "mfma", "unit": "TFLOP/s", "peak": PEAK_F64_TFLOPS,

@@ -216,6 +216,15 @@ int mepol_policy_forward(const double* x, int64_t n, int in_features, const doub
                          const double* actions, int action_dim, double* h1_out, double* z2_out,
                          double* mu_out, double* logp_out, void* stream);
 
+/* mepol_policy_forward plus relu'(h1) as bits: h1_mask_out [n, ceil(hidden0 / 16)] uint16,
+ * bit b of word w of row r = (h1[r][16 w + b] > 0), for mepol_dh1_layer1_backward_masked. */
+int mepol_policy_forward_masked(const double* x, int64_t n, int in_features, const double* W1,
+                                const double* b1, int hidden0, const double* W2, const double* b2,
+                                int hidden1, const double* Wm, const double* bm,
+                                const double* log_std, const double* actions, int action_dim,
+                                double* h1_out, double* z2_out, double* mu_out, double* logp_out,
+                                uint16_t* h1_mask_out, void* stream);
+
 /* Backward of the first layer fused into the dh1 GEMM: dW1 [h0, in] and db1 [h0] (nullable) of
  * h1 = relu(x W1^T + b1) from dz2 [n, k] and W2t = W2^T [h0, k] (dh1 = dz2 W2 stays on chip,
  * masked by h1 > 0 from the forward's h1 [n, h0]).  k even, in_features <= 63, dz2 and W2t
@@ -226,6 +235,12 @@ int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double*
                               const double* h1, const double* x, int in_features, double* dW1,
                               double* db1, void* workspace, size_t workspace_bytes,
                               void* stream);
+/* The same with relu'(h1) from the forward's bit mask (mepol_policy_forward_masked) instead of
+ * the f64 h1 values: identical results, 1/64 of the epilogue's operand bytes. */
+int mepol_dh1_layer1_backward_masked(const double* dz2, int64_t n, int k, const double* W2t,
+                                     int hidden0, const uint16_t* h1_mask, const double* x,
+                                     int in_features, double* dW1, double* db1, void* workspace,
+                                     size_t workspace_bytes, void* stream);
 
 /* Weight gradient of a linear layer over a tall batch: dW [out, in] = dy^T x with dy [n, out]
  * and x [n, in] row-major f64 (the policy's dW2 = dz2^T h1, K = n), split-K on the f64 matrix

@@ -64,6 +64,11 @@ SIGNATURES = {
     "mepol_dh1_layer1_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
     "mepol_dh1_layer1_backward": [_c_vp, _c_i64, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_int,
                                   _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
+    "mepol_dh1_layer1_backward_masked": [_c_vp, _c_i64, _c_int, _c_vp, _c_int, _c_vp, _c_vp,
+                                         _c_int, _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
+    "mepol_policy_forward_masked": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
+                                    _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
+                                    _c_vp, _c_vp, _c_vp, _c_vp],
     "mepol_gemm_nt": [_c_vp, _c_i64, _c_int, _c_i64, _c_vp, _c_int, _c_i64, _c_vp, _c_int, _c_vp,
                       _c_i64, _c_int, _c_vp],
     "mepol_step_mountaincar": [_c_vp, _c_vp, _c_i64, _c_i64, _c_vp],

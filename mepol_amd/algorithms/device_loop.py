@@ -123,6 +123,10 @@ class DeviceIteration:
                           and os.environ.get("MEPOL_FUSED_DH1", "1") != "0")
         self.neg_one = torch.full((), -1.0, **f64)
         self.W2t = torch.empty((W2.shape[1], W2.shape[0]), **f64) if self.fused_dh1 else None
+        # relu'(h1) as bits, written by the fused forward beside h1 and read by the fused dh1
+        # backward in place of h1 (1/64 of the bytes its epilogue waits for)
+        self.h1_mask = (ops.h1_mask_buffer(self.N, W1.shape[0], dev)
+                        if self.fused_fwd and self.fused_dh1 else None)
         # every body takes its optimizer step through _optim_step, which leaves theta_t in the
         # replay's shadow (off_policy_optimization then copies it into last_valid only when it
         # needs it, not after every accepted step)
@@ -275,7 +279,7 @@ class DeviceIteration:
         W1, b1, W2, b2, Wm, bm, ls = self.named
         if self.fused_fwd:  # layer 1 + z2 GEMM + head in one kernel
             ops.policy_forward(self.x, W1, b1, W2, b2, Wm, bm, ls, self.act, self.h1, self.z2,
-                               self.mu, self.logp)
+                               self.mu, self.logp, mask_out=self.h1_mask)
             return
         ops.layer_forward(self.x, W1, b1, out=self.h1)
         torch.mm(self.h1, W2.t(), out=self.z2)
@@ -319,6 +323,7 @@ class DeviceIteration:
             if self.fused_dh1:  # dh1 stays on chip (csrc/gemm.hip)
                 dh1 = None
                 dW1, db1 = ops.dh1_layer1_backward(dz2, W2t, self.h1, self.x, ws=self.ws_dh1,
+                                                   mask=self.h1_mask,
                                                    dW_out=o[0], db_out=o[1])
             else:
                 dh1 = torch.mm(dz2, W2)

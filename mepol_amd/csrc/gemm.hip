@@ -12,6 +12,8 @@
 // give a lane all of its fragment data for the tile.
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace mepol {
 namespace gemm {
 
@@ -184,10 +186,14 @@ constexpr int WR = 8, WC = 1, FR = 2, FC = 5;
 using P = Cfg<WR, WC, FR, FC>;
 }  // namespace l1b
 
-template <int NH>  // NH = ceil((F + 1) / 16) column groups of [x | 1]
+// MASK: relu'(h1) comes as the forward's bit mask (uint16 word kt of row r holds
+// h1[r][16 kt + b] > 0 in bit b, mepol_policy_forward_masked) instead of the f64 h1 values:
+// 2 B per 16 columns instead of 128 B, which the epilogue waited for with the MFMAs idle
+// (one workgroup per CU).  The same bits either way.
+template <int NH, bool MASK>  // NH = ceil((F + 1) / 16) column groups of [x | 1]
 __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
     const double* __restrict__ dz2, int64_t N, int K, const double* __restrict__ W2t, int M,
-    const double* __restrict__ h1, const double* __restrict__ x, int F,
+    const void* __restrict__ h1v, const double* __restrict__ x, int F,
     double* __restrict__ part) {
   using namespace l1b;
   constexpr int BM = P::BM, BN = P::BN, T = P::kThreads;
@@ -208,7 +214,11 @@ __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
   // (0.40 of the kernel's 1.23 ms went to this epilogue, profiles/r5/f64/).
   // B operands [x | 1] for k-step (i, q): lane (fr, g) holds x[row(i, q, g)][16 h + fr]
   double xb[FR][4][NH];
-  double hv[FC][FR][4];
+  using HT = typename std::conditional<MASK, uint32_t, double>::type;
+  HT hv[FC][FR][4];
+  const double* h1 = static_cast<const double*>(h1v);
+  const uint16_t* hm = static_cast<const uint16_t*>(h1v);
+  const int mw = (M + 15) / 16;
 #pragma unroll
   for (int i = 0; i < FR; ++i)
 #pragma unroll
@@ -217,11 +227,17 @@ __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
       // k-step (i, q): rows 16 i + 4 q + g
       const int64_t r = row0 + wave * FR * 16 + i * 16 + 4 * q + g;
       const double* xr = x + min<int64_t>(r, N - 1) * F;
-      const double* hr = h1 + min<int64_t>(r, N - 1) * M;
 #pragma unroll
       for (int h = 0; h < NH; ++h) xb[i][q][h] = xr[min(16 * h + fr, F - 1)];
+      if constexpr (MASK) {
+        const uint16_t* mr = hm + min<int64_t>(r, N - 1) * mw;
 #pragma unroll
-      for (int j = 0; j < FC; ++j) hv[j][i][q] = hr[min(col0 + j * 16 + fr, M - 1)];
+        for (int j = 0; j < FC; ++j) hv[j][i][q] = mr[min((col0 >> 4) + j, mw - 1)];
+      } else {
+        const double* hr = h1 + min<int64_t>(r, N - 1) * M;
+#pragma unroll
+        for (int j = 0; j < FC; ++j) hv[j][i][q] = hr[min(col0 + j * 16 + fr, M - 1)];
+      }
     }
 #pragma unroll
   for (int i = 0; i < FR; ++i)
@@ -249,7 +265,12 @@ __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
     for (int i = 0; i < FR; ++i)
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const double dz = (hv[j][i][q] > 0.0 && c < M) ? acc[i][j][q] : 0.0;
+        bool on;
+        if constexpr (MASK)
+          on = ((hv[j][i][q] >> fr) & 1u) != 0;
+        else
+          on = hv[j][i][q] > 0.0;
+        const double dz = (on && c < M) ? acc[i][j][q] : 0.0;
 #pragma unroll
         for (int h = 0; h < NH; ++h)
           dacc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(dz, xb[i][q][h], dacc[h], 0, 0, 0);
@@ -377,10 +398,11 @@ extern "C" int mepol_dh1_layer1_workspace_size(int64_t n, int m, int in_features
   return 0;
 }
 
-extern "C" int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double* W2t,
-                                         int m, const double* h1, const double* x,
-                                         int in_features, double* dW1, double* db1,
-                                         void* workspace, size_t workspace_bytes, void* stream) {
+template <bool MASK>
+static int dh1_layer1_backward(const double* dz2, int64_t n, int k, const double* W2t, int m,
+                               const void* h1, const double* x, int in_features, double* dW1,
+                               double* db1, void* workspace, size_t workspace_bytes,
+                               void* stream) {
   using namespace mepol::gemm::l1b;
   using mepol::gemm::dh1_layer1_bwd_kernel;
   const int F = in_features;
@@ -405,11 +427,12 @@ extern "C" int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, co
   do {                                                                                         \
     static bool attr = false;                                                                  \
     if (!attr) {                                                                               \
-      MEPOL_HIP(hipFuncSetAttribute((const void*)dh1_layer1_bwd_kernel<NHV>,                   \
+      MEPOL_HIP(hipFuncSetAttribute((const void*)dh1_layer1_bwd_kernel<NHV, MASK>,             \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)P::kLds)); \
       attr = true;                                                                             \
     }                                                                                          \
-    hipLaunchKernelGGL(dh1_layer1_bwd_kernel<NHV>, dim3(tiles), dim3(P::kThreads), P::kLds, st, \
+    hipLaunchKernelGGL((dh1_layer1_bwd_kernel<NHV, MASK>), dim3(tiles), dim3(P::kThreads),      \
+                       P::kLds, st,                                                            \
                        dz2, n, k, W2t, m, h1, x, F, part);                                     \
   } while (0)
   switch (nh) {
@@ -430,4 +453,22 @@ extern "C" int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, co
                      dim3(256), 0, st, grp, m, F, dW1, db1);
   MEPOL_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int mepol_dh1_layer1_backward(const double* dz2, int64_t n, int k, const double* W2t,
+                                         int m, const double* h1, const double* x,
+                                         int in_features, double* dW1, double* db1,
+                                         void* workspace, size_t workspace_bytes, void* stream) {
+  return dh1_layer1_backward<false>(dz2, n, k, W2t, m, h1, x, in_features, dW1, db1, workspace,
+                                    workspace_bytes, stream);
+}
+
+extern "C" int mepol_dh1_layer1_backward_masked(const double* dz2, int64_t n, int k,
+                                                const double* W2t, int m,
+                                                const uint16_t* h1_mask, const double* x,
+                                                int in_features, double* dW1, double* db1,
+                                                void* workspace, size_t workspace_bytes,
+                                                void* stream) {
+  return dh1_layer1_backward<true>(dz2, n, k, W2t, m, h1_mask, x, in_features, dW1, db1,
+                                   workspace, workspace_bytes, stream);
 }

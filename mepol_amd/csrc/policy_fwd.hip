@@ -45,7 +45,8 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
     const double* __restrict__ b2, int H2, const double* __restrict__ Wm,
     const double* __restrict__ bm, const double* __restrict__ log_std,
     const double* __restrict__ act, int A, double* __restrict__ h1_out,
-    double* __restrict__ z2_out, double* __restrict__ mu_out, double* __restrict__ logp_out) {
+    double* __restrict__ z2_out, double* __restrict__ mu_out, double* __restrict__ logp_out,
+    uint16_t* __restrict__ mask_out) {
   constexpr int XP = FP + 2;  // padded x row: lanes of a fragment read hit distinct banks
   extern __shared__ double lds[];
   double* sA = lds;                    // [2][BM][KP]  h1 k-tile (A operand)
@@ -105,12 +106,18 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
     for (int u = 1; u < NCH; ++u) h += hc[u];
     const int c = kt * KT + fr;
     const double bc = c < H1 ? b1[c] : 0.0;
+    const int mw = (H1 + 15) / 16;  // mask row stride (16-bit words)
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int r = wave * 16 + g + 4 * q;
       const double v = c < H1 ? fmax(h[q] + bc, 0.0) : 0.0;
       sA[(buf * BM + r) * KP + fr] = v;
       if (c < H1 && row0 + r < N) h1_out[(row0 + r) * H1 + c] = v;
+      // relu'(h1) as bits for the backward (dh1's epilogue reads 2 B per 16 columns instead
+      // of the 8-B h1 values): bit fr of word kt of row r = (h1[r][16 kt + fr] > 0)
+      const uint64_t bits = __ballot(v > 0.0);
+      if (mask_out && fr == 0 && row0 + r < N)
+        mask_out[(row0 + r) * mw + kt] = (uint16_t)(bits >> (16 * g));
     }
   };
 
@@ -295,7 +302,7 @@ template <int FP, bool VEC>
 int launch(const double* x, int64_t n, int F, const double* W1, const double* b1, int H1,
            const double* W2, const double* b2, int H2, const double* Wm, const double* bm,
            const double* log_std, const double* act, int A, double* h1, double* z2, double* mu,
-           double* logp, hipStream_t st) {
+           double* logp, uint16_t* mask, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     MEPOL_HIP(hipFuncSetAttribute((const void*)policy_fwd_kernel<FP, VEC>,
@@ -305,7 +312,8 @@ int launch(const double* x, int64_t n, int F, const double* W1, const double* b1
   }
   const unsigned blocks = (unsigned)((n + BM - 1) / BM);
   hipLaunchKernelGGL((policy_fwd_kernel<FP, VEC>), dim3(blocks), dim3(kThreads), lds_bytes<FP>(), st,
-                     x, n, F, W1, b1, H1, W2, b2, H2, Wm, bm, log_std, act, A, h1, z2, mu, logp);
+                     x, n, F, W1, b1, H1, W2, b2, H2, Wm, bm, log_std, act, A, h1, z2, mu, logp,
+                     mask);
   MEPOL_CHECK_LAUNCH();
   return 0;
 }
@@ -313,13 +321,12 @@ int launch(const double* x, int64_t n, int F, const double* W1, const double* b1
 }  // namespace pfwd
 }  // namespace mepol
 
-extern "C" int mepol_policy_forward(const double* x, int64_t n, int in_features,
-                                    const double* W1, const double* b1, int hidden0,
-                                    const double* W2, const double* b2, int hidden1,
-                                    const double* Wm, const double* bm, const double* log_std,
-                                    const double* actions, int action_dim, double* h1_out,
-                                    double* z2_out, double* mu_out, double* logp_out,
-                                    void* stream) {
+static int policy_forward(const double* x, int64_t n, int in_features, const double* W1,
+                          const double* b1, int hidden0, const double* W2, const double* b2,
+                          int hidden1, const double* Wm, const double* bm,
+                          const double* log_std, const double* actions, int action_dim,
+                          double* h1_out, double* z2_out, double* mu_out, double* logp_out,
+                          uint16_t* h1_mask_out, void* stream) {
   using namespace mepol::pfwd;
   if (n < 0 || in_features <= 0 || in_features > 64 || hidden0 <= 0 || hidden1 <= 0 ||
       hidden1 > BN || action_dim <= 0 || !x || !W1 || !b1 || !W2 || !b2 || !Wm || !bm ||
@@ -335,10 +342,10 @@ extern "C" int mepol_policy_forward(const double* x, int64_t n, int in_features,
   return (hidden0 % 2 == 0 && hidden0 >= 2)                                                  \
              ? launch<FPV, true>(x, n, in_features, W1, b1, hidden0, W2, b2, hidden1, Wm, bm, \
                                  log_std, actions, action_dim, h1_out, z2_out, mu_out,        \
-                                 logp_out, st)                                                \
+                                 logp_out, h1_mask_out, st)                                   \
              : launch<FPV, false>(x, n, in_features, W1, b1, hidden0, W2, b2, hidden1, Wm,    \
                                   bm, log_std, actions, action_dim, h1_out, z2_out, mu_out,   \
-                                  logp_out, st)
+                                  logp_out, h1_mask_out, st)
   if (in_features <= 4) MEPOL_PF(4);
   if (in_features <= 8) MEPOL_PF(8);
   if (in_features <= 16) MEPOL_PF(16);
@@ -346,4 +353,32 @@ extern "C" int mepol_policy_forward(const double* x, int64_t n, int in_features,
   if (in_features <= 48) MEPOL_PF(48);
   MEPOL_PF(64);
 #undef MEPOL_PF
+}
+
+extern "C" int mepol_policy_forward(const double* x, int64_t n, int in_features,
+                                    const double* W1, const double* b1, int hidden0,
+                                    const double* W2, const double* b2, int hidden1,
+                                    const double* Wm, const double* bm, const double* log_std,
+                                    const double* actions, int action_dim, double* h1_out,
+                                    double* z2_out, double* mu_out, double* logp_out,
+                                    void* stream) {
+  return policy_forward(x, n, in_features, W1, b1, hidden0, W2, b2, hidden1, Wm, bm, log_std,
+                        actions, action_dim, h1_out, z2_out, mu_out, logp_out, nullptr, stream);
+}
+
+extern "C" int mepol_policy_forward_masked(const double* x, int64_t n, int in_features,
+                                           const double* W1, const double* b1, int hidden0,
+                                           const double* W2, const double* b2, int hidden1,
+                                           const double* Wm, const double* bm,
+                                           const double* log_std, const double* actions,
+                                           int action_dim, double* h1_out, double* z2_out,
+                                           double* mu_out, double* logp_out,
+                                           uint16_t* h1_mask_out, void* stream) {
+  if (!h1_mask_out) {
+    mepol::set_error("mepol_policy_forward_masked: h1_mask_out is null");
+    return mepol::kErrBadArg;
+  }
+  return policy_forward(x, n, in_features, W1, b1, hidden0, W2, b2, hidden1, Wm, bm, log_std,
+                        actions, action_dim, h1_out, z2_out, mu_out, logp_out, h1_mask_out,
+                        stream);
 }

@@ -371,11 +371,17 @@ def policy_forward_ok(in_features, hidden1):
     return in_features <= POLICY_FWD_MAX_IN and hidden1 <= POLICY_FWD_MAX_H1
 
 
+def h1_mask_buffer(n, hidden0, device):
+    """relu'(h1) bit mask of policy_forward(mask_out=...): [n, ceil(hidden0 / 16)] int16."""
+    return torch.empty((n, (hidden0 + 15) // 16), dtype=torch.int16, device=device)
+
+
 def policy_forward(x, W1, b1, W2, b2, Wm, bm, log_std, act, h1_out=None, z2_out=None,
-                   mu_out=None, logp_out=None):
+                   mu_out=None, logp_out=None, mask_out=None):
     """One-kernel forward of the two-hidden-layer Gaussian policy: returns (h1, z2, mu, logp)
     with h1 = relu(x W1^T + b1), z2 = h1 W2^T (pre-bias), mu = relu(z2 + b2) Wm^T + bm and
-    logp = sum_a log N(act | mu, exp(log_std) + 1e-7)."""
+    logp = sum_a log N(act | mu, exp(log_std) + 1e-7).  With mask_out (h1_mask_buffer) the
+    kernel also writes relu'(h1) as bits for dh1_layer1_backward(mask=...)."""
     n, f = x.shape
     h0, h1w, a = W1.shape[0], W2.shape[0], Wm.shape[0]
     dev = x.device
@@ -387,9 +393,16 @@ def policy_forward(x, W1, b1, W2, b2, Wm, bm, log_std, act, h1_out=None, z2_out=
     z2 = buf(z2_out, (n, h1w))
     mu = buf(mu_out, (n, a))
     logp = buf(logp_out, (n,))
-    call("mepol_policy_forward", ptr(x), n, f, ptr(W1), ptr(b1), h0, ptr(W2), ptr(b2), h1w,
-         ptr(Wm), ptr(bm), ptr(log_std), ptr(act), a, ptr(h1), ptr(z2), ptr(mu), ptr(logp),
-         _stream())
+    if mask_out is None:
+        call("mepol_policy_forward", ptr(x), n, f, ptr(W1), ptr(b1), h0, ptr(W2), ptr(b2), h1w,
+             ptr(Wm), ptr(bm), ptr(log_std), ptr(act), a, ptr(h1), ptr(z2), ptr(mu), ptr(logp),
+             _stream())
+    else:
+        assert mask_out.shape == (n, (h0 + 15) // 16) and mask_out.dtype == torch.int16
+        assert mask_out.is_contiguous()
+        call("mepol_policy_forward_masked", ptr(x), n, f, ptr(W1), ptr(b1), h0, ptr(W2), ptr(b2),
+             h1w, ptr(Wm), ptr(bm), ptr(log_std), ptr(act), a, ptr(h1), ptr(z2), ptr(mu),
+             ptr(logp), ptr(mask_out), _stream())
     return h1, z2, mu, logp
 
 
@@ -400,7 +413,7 @@ def dh1_layer1_ok(in_features, hidden1):
     return in_features <= DH1_L1_MAX_IN and hidden1 % 2 == 0
 
 
-def dh1_layer1_backward(dz2, W2t, h1, x, ws=None, dW_out=None, db_out=None):
+def dh1_layer1_backward(dz2, W2t, h1, x, ws=None, dW_out=None, db_out=None, mask=None):
     """(dW1, db1) of h1 = relu(x W1^T + b1) from dz2 = dL/dz2 [n, h1w] and W2t = W2^T
     [h0, h1w]: dh1 = dz2 W2 is reduced on chip (csrc/gemm.hip), never written."""
     n, k = dz2.shape
@@ -417,8 +430,13 @@ def dh1_layer1_backward(dz2, W2t, h1, x, ws=None, dW_out=None, db_out=None):
                                                       device=x.device)
     db = db_out if db_out is not None else torch.empty(h0, dtype=torch.float64, device=x.device)
     assert dW.is_contiguous() and db.is_contiguous()
-    call("mepol_dh1_layer1_backward", ptr(dz2), n, k, ptr(W2t), h0, ptr(h1), ptr(x), f, ptr(dW),
-         ptr(db), ptr(ws), ws.numel(), _stream())
+    if mask is None:
+        call("mepol_dh1_layer1_backward", ptr(dz2), n, k, ptr(W2t), h0, ptr(h1), ptr(x), f,
+             ptr(dW), ptr(db), ptr(ws), ws.numel(), _stream())
+    else:  # relu'(h1) from the forward's bit mask (policy_forward(mask_out=...))
+        assert mask.shape == (n, (h0 + 15) // 16) and mask.dtype == torch.int16
+        call("mepol_dh1_layer1_backward_masked", ptr(dz2), n, k, ptr(W2t), h0, ptr(mask),
+             ptr(x), f, ptr(dW), ptr(db), ptr(ws), ws.numel(), _stream())
     return dW, db
 
 

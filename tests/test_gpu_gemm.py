@@ -51,3 +51,33 @@ def test_dh1_layer1_backward_matches_torch(cuda, n, nf, h0, h1w):
     dz1 = (dz2 @ W2) * (h1 > 0)
     torch.testing.assert_close(dW1, dz1.t() @ x, rtol=1e-11, atol=1e-11)
     torch.testing.assert_close(db1, dz1.sum(0), rtol=1e-11, atol=1e-11)
+
+
+@pytest.mark.parametrize("n,nf,h0,h1w,a", [(200000, 29, 400, 300, 8), (20000, 2, 300, 300, 2),
+                                           (4097, 47, 400, 300, 17), (333, 5, 37, 46, 3),
+                                           (1000, 63, 400, 300, 20)])
+def test_h1_mask_and_masked_dh1(cuda, n, nf, h0, h1w, a):
+    """policy_forward(mask_out=...) writes relu'(h1) as bits (word w of row r, bit b:
+    h1[r][16 w + b] > 0) and dh1_layer1_backward(mask=...) gives the same bits as the h1 path."""
+    from mepol_amd import ops
+
+    torch.manual_seed(n + h0)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    x = torch.randn(n, nf, **f64)
+    W1, b1 = torch.randn(h0, nf, **f64) * 0.3, torch.randn(h0, **f64) * 0.1
+    W2, b2 = torch.randn(h1w, h0, **f64) * 0.1, torch.randn(h1w, **f64) * 0.1
+    Wm, bm = torch.randn(a, h1w, **f64) * 0.1, torch.randn(a, **f64)
+    ls = torch.full((a,), -0.5, **f64)
+    act = torch.randn(n, a, **f64)
+    mask = ops.h1_mask_buffer(n, h0, x.device)
+    h1, z2, mu, lp = ops.policy_forward(x, W1, b1, W2, b2, Wm, bm, ls, act, mask_out=mask)
+    h1r, z2r, mur, lpr = ops.policy_forward(x, W1, b1, W2, b2, Wm, bm, ls, act)
+    assert torch.equal(h1, h1r) and torch.equal(z2, z2r) and torch.equal(lp, lpr)
+    pos = torch.nn.functional.pad(h1 > 0, (0, mask.shape[1] * 16 - h0)).view(n, -1, 16)
+    want = (pos.to(torch.int32) << torch.arange(16, device="cuda", dtype=torch.int32)).sum(-1)
+    assert torch.equal(mask.to(torch.int32) & 0xFFFF, want)
+    dz2 = torch.randn(n, h1w, **f64)
+    W2t = W2.t().contiguous()
+    dW1, db1 = ops.dh1_layer1_backward(dz2, W2t, h1, x)
+    dW1m, db1m = ops.dh1_layer1_backward(dz2, W2t, h1, x, mask=mask)
+    assert torch.equal(dW1, dW1m) and torch.equal(db1, db1m)
