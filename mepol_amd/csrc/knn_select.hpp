@@ -76,7 +76,7 @@ __device__ __forceinline__ void flush_groups(float (&ld)[LIST], int (&li)[LIST],
 // One query tile of 32 per wave (one lane = one query column, 16 of each candidate tile's 32
 // rows), four waves per workgroup.  The candidate fragments stream from L2 into every wave
 // (1 KB per k-step, half and tile): at C3 the texture data path is the bound (TD busy ~ the
-// kernel's CU-cycles, profiles/r5/knn/select_counters_C3.txt).  Tried and dropped in round 5
+// kernel's CU-cycles, profiles/r5/knn/select_counters_C3_*.txt).  Tried and dropped in round 5
 // (profiles/r5/knn/): two query tiles per wave (the lists then cap occupancy at 2 waves per
 // SIMD), and the fragments shared through an LDS ring (3x less texture traffic, but a barrier
 // per ring interval made the waves wait out each other's insertions; tools/variants/).
