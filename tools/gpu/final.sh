@@ -25,3 +25,8 @@ cat "$out/bench_prof.json"
 echo "[final] bench C3R8"
 timeout -k 10 300 python -u bench.py --workload C3R8 --no-cpu-baseline > "$out/bench_C3R8.json" 2> "$out/bench_C3R8.err" || { tail -20 "$out/bench_C3R8.err"; exit 1; }
 cat "$out/bench_C3R8.json"
+echo "[final] select counters"
+timeout -k 10 400 bash tools/gpu/sel_counters.sh "$(basename $out)/sel" > "$out/sel.log" 2>&1 || { tail -20 "$out/sel.log"; exit 1; }
+echo "[final] MLP counters"
+timeout -k 10 400 bash tools/gpu/mlp_counters.sh "$(basename $out)/mlp" > "$out/mlp.log" 2>&1 || { tail -20 "$out/mlp.log"; exit 1; }
+tail -3 "$out/mlp.log"
