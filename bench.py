@@ -656,8 +656,11 @@ def cpu_baseline(cfg, sample_queries, iters_done):
     kl_s = time.perf_counter() - t
     iters = float(np.mean(iters_done)) if iters_done else float(cfg["max_off_iters"])
     epoch_s = roll_s + knn_s + iters * (upd_s + kl_s) + kl_s
-    sample = (f"sklearn {sklearn.__version__} NearestNeighbors(auto, n_jobs={cores}) on {nq} of "
-              f"{N} queries x {N} candidates (scaled x{N / nq:.1f}) = {knn_s:.2f} s; one "
+    algo = nbrs._fit_method  # what 'auto' chose here (brute above d = 15 in sklearn >= 1.x)
+    sample = (f"sklearn {sklearn.__version__} NearestNeighbors(auto -> {algo}, n_jobs={cores}) on "
+              f"{nq} of {N} queries x {N} candidates (scaled x{N / nq:.1f}) = {knn_s:.2f} s "
+              f"(generous to the CPU where 'auto' picks brute: the reference pins sklearn 0.22, "
+              f"whose 'auto' picks kd_tree, far slower in high d); one "
               f"policy_update {upd_s:.2f} s + compute_kl {kl_s:.2f} s at full N "
               f"(x{iters:g} + final H)")
     if roll_s:
