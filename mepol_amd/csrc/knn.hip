@@ -242,7 +242,9 @@ __global__ __launch_bounds__(256) void refine_kernel(
   constexpr int kRM = MAXP <= 4 ? MAXP : 1;  // rank merge for M <= 256 entries
   __shared__ float2 sent[4][64 * kRM];        // rank merge: the query's entries (value, index bits)
   if (MAXP > 4) rank_merge = 0;
-  const int w = threadIdx.x >> 6;
+  // wave-uniform in an SGPR: the query row and the lists' addresses are then scalar, and the
+  // query's coordinates come through scalar loads instead of 64-lane broadcast vector loads
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int l = threadIdx.x & 63;
   // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs, so block b runs on
   // XCD b % 8; each XCD gets one contiguous range of query blocks.  Neighbouring queries' rows of
