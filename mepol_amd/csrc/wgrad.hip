@@ -16,26 +16,34 @@
 // iteration's dW2: 1.04 ms + reduce at C3 (46 TF/s on 48 GF).
 #include "common.hpp"
 
+#include <algorithm>
+
 namespace mepol {
 namespace wgrad {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int FO = 4, FI = 5;      // 16 x 16 fragments per wave: 64 (o) x 80 (i)
+constexpr int kOcc = 2;            // waves per SIMD (VGPR budget 256)
 constexpr int BO = 16 * FO, BI = 16 * FI;
 constexpr int NL = FO + FI;        // operand loads per lane and k-step
-// k-steps of operands in the register ring (3 spills at this tile; 64 x 64 tiles with 3
-// measured slower: tools/wgrad_probe.py, profiles/r5/f64/wgrad_probe.txt)
+// k-steps of operands in the register ring (3 spills at this tile).  Measured slower
+// (tools/wgrad_probe.py, profiles/r5/f64/wgrad_probe.txt): 64 x 64 tiles with 3 stages, and
+// 80 x 80 tiles at one wave per SIMD with 2 or 3 stages.
 constexpr int NS = 2;
-constexpr int kMaxSlices = 80;
+constexpr int kMaxSlices = 128;
 constexpr int kSliceRowsMin = 256;
 
-__host__ __device__ inline int slices_for(int64_t n) {
-  int64_t s = n / kSliceRowsMin;
-  s = s < 8 ? 8 : (s > kMaxSlices ? kMaxSlices : s);
-  return (int)(s & ~7);  // a multiple of 8: the slice -> XCD map below has no idle blocks
+// K-slices: enough (tile, slice) waves for one full round on the 1024 SIMDs at the kernel's
+// occupancy, in multiples of 8 (the slice -> XCD map below has no idle blocks), and no slice
+// shorter than kSliceRowsMin rows.
+inline int slices_for(int64_t n, int O, int I) {
+  const int64_t ntile = (int64_t)((O + BO - 1) / BO) * ((I + BI - 1) / BI);
+  int64_t s = std::max<int64_t>(8, 1024 * kOcc / ntile);
+  s = std::min<int64_t>(s, std::max<int64_t>(8, n / kSliceRowsMin));
+  return (int)std::min<int64_t>(kMaxSlices, s & ~7);
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void wgrad_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kOcc))) void wgrad_kernel(
     const double* __restrict__ dy, int64_t n, int O, const double* __restrict__ x, int I,
     int nob, int nib, int S, int64_t slice_rows, double* __restrict__ part) {
   // block b -> (slice, tile): blocks b and b + 8 share an XCD under the round-robin dispatch,
@@ -158,7 +166,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const double* __restr
 extern "C" int mepol_weight_grad_workspace_size(int64_t n, int out_features, int in_features,
                                                 size_t* bytes) {
   if (!bytes || n < 0 || out_features <= 0 || in_features <= 0) return mepol::kErrBadArg;
-  *bytes = (size_t)mepol::wgrad::slices_for(n) * out_features * in_features * sizeof(double);
+  *bytes = (size_t)mepol::wgrad::slices_for(n, out_features, in_features) * out_features *
+           in_features * sizeof(double);
   return 0;
 }
 
@@ -171,7 +180,7 @@ extern "C" int mepol_weight_grad(const double* dy, int64_t n, int out_features, 
     mepol::set_error("mepol_weight_grad: bad arguments");
     return mepol::kErrBadArg;
   }
-  const int S = slices_for(n);
+  const int S = slices_for(n, O, I);
   const size_t need = (size_t)S * O * I * sizeof(double);
   if (workspace_bytes < need) {
     mepol::set_error("mepol_weight_grad: workspace %zu < %zu", workspace_bytes, need);
