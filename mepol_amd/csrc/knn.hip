@@ -559,13 +559,14 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   P->nqt = (nq + 31) / 32;
   int split = split_hint;
   if (split <= 0) {
-    // About 2500 query-tile waves (0.8 of the 3072 wave slots at 3 waves per SIMD), tiles
+    // About 1600 query-tile waves (half of the 3072 wave slots at 3 waves per SIMD), tiles
     // >= 16 per split.  Every (query, split) pays the list warm-up (the prune bound starts at
-    // +inf) and refine ranks 2 split LIST16 entries per query, so fewer, longer ranges win even
-    // below a full chip: 25k queries x 200k (the C3 shard at 8 ranks) take 1.93 ms at split 5,
-    // 1.66 at 2-3; 200k queries 7.9 ms at 2, 9.5 at 4 (profiles/r4/knn/splits.log).  The lists
-    // keep >= 2 ranges (one range of half lists certifies too few queries).
-    const int64_t target = 2500;
+    // +inf, or at a finished range's bound) and refine ranks 2 split LIST16 entries per query,
+    // so fewer, longer ranges win even below a full chip: 25k queries x 200k (the C3 shard at
+    // 8 ranks) take 1.25 ms at split 2, 1.30 at 3, 1.54 at 4, 1.94 at 8; 200k queries 5.27 ms at
+    // 2, 5.62 at 3, 5.97 at 4 (round 5, profiles/r5/knn/splits.txt).  The lists keep >= 2
+    // ranges (one range of half lists certifies too few queries).
+    const int64_t target = 1600;
     split = (int)std::min<int64_t>(kMaxSplit, std::max<int64_t>(1, (target + P->nqt / 2) /
                                                                       std::max<int64_t>(P->nqt, 1)));
     split = std::max(split, 2);
