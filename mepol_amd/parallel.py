@@ -109,13 +109,17 @@ class ShardedEpoch:
         self.D, self.I, self.idx32T, check = self.ops.knn(cand, self.k + 1,
                                                           query=self.next_states,
                                                           defer_check=True)
-        # rejected input on any rank: every rank's k-NN kernels returned early, and the
-        # gathered idx rows below are undefined, so each rank raises before using them
-        check.raise_if_invalid()
         idx_all = self._gather(self.idx32T[: self.k].contiguous())       # [G, k, n_local]
         idx_allT = idx_all.permute(1, 0, 2).reshape(self.k, self.N).contiguous()
         self.csr = self.ops.csr_build(idx_allT, self.k, self.n_local, col_offset=self.R0,
                                       row_offset=0, nq=self.N)
+        # The input check is read only now, with the gather and the CSR build queued behind
+        # the k-NN (one host wait less in the epoch set-up).  A rejected input (a NaN / inf
+        # coordinate) is rejected on every rank alike -- the check covers the gathered
+        # candidates, which every rank holds -- so all ranks issued the same gather and all
+        # raise here; the k-NN kernels returned early, the gathered rows are undefined and the
+        # CSR build (which bounds-checks its ids) is discarded with them.
+        check.raise_if_invalid()
         return self.D, self.I
 
     # -- policy log-probs -----------------------------------------------------------------------

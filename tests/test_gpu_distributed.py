@@ -105,3 +105,44 @@ def test_two_ranks_on_one_gpu_match_single_rank(cuda, tmp_path):
     np.testing.assert_allclose(r2["hs"], hs, rtol=1e-12)
     np.testing.assert_allclose(r2["kls"], kls, rtol=1e-9, atol=1e-14)
     np.testing.assert_allclose(r2["params"], p, rtol=1e-9, atol=1e-12)
+
+
+class _OneRank:
+    """A one-rank stand-in for torch.distributed (ShardedEpoch's collectives are then copies)."""
+
+    def get_world_size(self, group=None):
+        return 1
+
+    def get_rank(self, group=None):
+        return 0
+
+    def get_backend(self, group=None):
+        return "gloo"
+
+    def all_gather_into_tensor(self, out, inp, group=None):
+        out.copy_(inp.reshape(-1))
+
+    def all_reduce(self, t, op=None, group=None):
+        return None
+
+
+def test_sharded_knn_rejects_nan(cuda):
+    """The sharded epoch reads the k-NN input check after the gather and the CSR build are
+    queued: a NaN state must still raise (MepolInputError, a ValueError, as sklearn) and leave
+    no partial epoch behind."""
+    from mepol_amd._lib import MepolInputError
+    from mepol_amd.parallel import ShardedEpoch
+
+    states, actions = _data()
+    dev = torch.device("cuda:0")
+    st = torch.as_tensor(states, dtype=torch.float64, device=dev)
+    ac = torch.as_tensor(actions, dtype=torch.float64, device=dev)
+    rtl = torch.full((NT, 1), T, dtype=torch.int64, device=dev)
+    nxt = torch.as_tensor(states[:, 1:].reshape(-1, NF), device=dev)
+    bad = nxt.clone()
+    bad[7, 1] = float("nan")
+    with pytest.raises(MepolInputError):
+        ShardedEpoch(st, ac, rtl, bad, K, _OneRank()).build_knn()
+    ep = ShardedEpoch(st, ac, rtl, nxt, K, _OneRank())
+    D, I = ep.build_knn()
+    assert torch.isfinite(D).all()
