@@ -16,7 +16,10 @@ struct LaneList {
   int cnt;
 };
 
-constexpr int kGrpCap = 8;  // row-group entries per lane in the LDS group buffer
+// Row-group entries per lane in the LDS group buffer: 10 (51.2 KB per workgroup, still 3 per
+// CU); a fuller buffer makes fuller flushes: C3 select 4.96 -> 4.78 ms against 8, 5.43 at 6
+// (profiles/r5/knn/grpcap_ab.txt)
+constexpr int kGrpCap = 10;
 
 // The lane's group buffer into its sorted list.  A hit row group is buffered whole (its four
 // values and the candidate index of its first row), so recording it costs the wave one address
