@@ -201,7 +201,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
           S.cnt += 1;
         }
       }
-      // a tile adds <= 4 entries: the cursor enters every tile at <= kGrpCap - 4
+      // a tile adds <= 4 entries: the cursor enters every tile at <= kGrpCap - 4 (a check per
+      // pair of row groups at kGrpCap - 2 measured slower: profiles/r5/knn/grpcap_ab.txt)
       if (__ballot(S.cnt > kGrpCap - 4))
         flush_groups<LIST>(S.ld, S.li, S.thr, S.cnt, gbv[w], gbt[w], l, S.thr0, keep);
     }
