@@ -489,7 +489,10 @@ static int make_exhaustive_plan(Plan* P) {
   return 0;
 }
 
-static const int kListChoices[] = {8, 16, 22, 24, 32, 40};  // 22 = keep + 4 at k + 1 = 31
+// 22 = keep + 4 at k + 1 = 31; keep + 2 (20 there) makes the select 3 % faster but sends 43
+// instead of 1 of 200k queries to the exhaustive stage, slower overall (round 5,
+// profiles/r5/knn/list_slack_ab.txt)
+static const int kListChoices[] = {8, 16, 20, 22, 24, 32, 40};
 
 static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Plan* P) {
   if (nc <= 0 || nq < 0 || d <= 0 || kp1 <= 0) {

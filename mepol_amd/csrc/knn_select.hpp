@@ -277,6 +277,7 @@ static void launch_select16_ks(const SelectArgs& a, hipStream_t st) {
   switch (a.LIST16) {  // >= keep + 4 >= 7; split-candidate plans keep the instances that fit
     case 8: MEPOL_SEL16(8, 3); break;
     case 16: MEPOL_SEL16(16, O3); break;
+    case 20: MEPOL_SEL16(20, O3); break;
     case 22: MEPOL_SEL16(22, O3); break;
     case 24: MEPOL_SEL16(24, O3); break;
     case 32: MEPOL_SEL16(32, 1); break;
