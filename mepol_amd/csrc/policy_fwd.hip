@@ -16,6 +16,12 @@
 // This replaces layer_forward + the z2 GEMM + head_forward (three passes over the N x h0 and
 // N x h1 activations) with one: the layer-1 recompute costs ceil4(nf)/320 of the GEMM's MFMA
 // work (10 % at nf = 29) and the head epilogue ~2 %.  Limits: nf <= 64, h1 (hidden[1]) <= 320.
+//
+// Round 5: with h0 even (every bench shape) the forward runs in a split form instead --
+// layer1_kernel (h1 + its bit mask to HBM) then z2_head_kernel (the z2 GEMM with both operands
+// read straight from L2 into the MFMA fragments: no LDS staging, no barrier in the K loop, and
+// this kernel's head epilogue).  C3: 1.19 ms against 1.32 for the one-kernel form below, which
+// stays for odd h0 (profiles/r5/f64/forward_split_ab.txt).
 #include "common.hpp"
 
 namespace mepol {
@@ -298,6 +304,240 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
   if (ea == 0 && row0 + er < N) logp_out[row0 + er] = lp;
 }
 
+// ---------------------------------------------------------------------------------------
+// Split form (hidden0 even): layer 1 alone, then z2 + head with no LDS operand staging.
+// ---------------------------------------------------------------------------------------
+// h1 = relu(x W1^T + b1) and its bit mask, one wave per 16 rows: the row's x fragment stays in
+// registers (k = 4 s + g), the 16-column tiles of W1 stream from L2, stores are whole 128-B
+// row segments.  HBM-write bound (h1 is N x h0 f64).
+template <int FP>
+__global__ __launch_bounds__(256) void layer1_kernel(const double* __restrict__ x, int64_t N,
+                                                     int F, const double* __restrict__ W1,
+                                                     const double* __restrict__ b1, int H1,
+                                                     double* __restrict__ h1_out,
+                                                     uint16_t* __restrict__ mask_out) {
+  constexpr int NS = FP / 4, NCH = NS < 4 ? NS : 4;
+  const int l = threadIdx.x & 63, fr = l & 15, g = l >> 4;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  if (r0 >= N) return;  // wave-uniform
+  double xv[NS];
+  const int64_t xr = min<int64_t>(r0 + fr, N - 1);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int f = 4 * s + g;
+    const double v = x[xr * F + min(f, F - 1)];
+    xv[s] = f < F ? v : 0.0;
+  }
+  const int nkt = (H1 + 15) / 16, mw = nkt;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int c = kt * 16 + fr;
+    const double* wr = W1 + (int64_t)min(c, H1 - 1) * F;
+    double wv[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int f = 4 * s + g;
+      const double v = wr[min(f, F - 1)];
+      wv[s] = f < F ? v : 0.0;
+    }
+    const double bc = b1[min(c, H1 - 1)];
+    d4 hc[NCH];
+#pragma unroll
+    for (int u = 0; u < NCH; ++u) hc[u] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      hc[s % NCH] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s], wv[s], hc[s % NCH], 0, 0, 0);
+    d4 h = hc[0];
+#pragma unroll
+    for (int u = 1; u < NCH; ++u) h += hc[u];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t r = r0 + g + 4 * q;
+      const double v = c < H1 ? fmax(h[q] + bc, 0.0) : 0.0;
+      if (c < H1 && r < N) h1_out[r * H1 + c] = v;
+      const uint64_t bits = __ballot(v > 0.0);
+      if (mask_out && fr == 0 && r < N) mask_out[r * mw + kt] = (uint16_t)(bits >> (16 * g));
+    }
+  }
+}
+
+// z2 = h1 W2^T and the head, one workgroup per 64-row block: wave w owns columns
+// [80 w, 80 w + 80) (4 x 5 fragments) and reads both operands straight from L2 into the MFMA
+// fragments -- a lane takes 16 B of its row per fragment, k = 8 st + 2 g + {0, 1}, and the
+// stage's two k-steps use the two halves (h1 and W2 in the same k order).  No LDS staging and
+// no barrier in the K loop; the head epilogue is the fused kernel's (LDS only for the sum of
+// the 4 column waves).  tools/z2_probe.py: the bare GEMM at 50.7 TF/s (C3) against 45 in the
+// fused kernel's k-tile loop.
+namespace zh {
+constexpr int FO = 4, FI = 5, NW = 4, NS = 2, NL = FO + FI;
+constexpr int BM = 16 * FO;  // rows per workgroup (x 320 columns)
+}  // namespace zh
+
+__global__ __launch_bounds__(64 * zh::NW) __attribute__((amdgpu_waves_per_eu(2))) void z2_head_kernel(
+    const double* __restrict__ h1, int64_t N, int H1, const double* __restrict__ W2,
+    const double* __restrict__ b2, int H2, const double* __restrict__ Wm,
+    const double* __restrict__ bm, const double* __restrict__ log_std,
+    const double* __restrict__ act, int A, double* __restrict__ z2_out,
+    double* __restrict__ mu_out, double* __restrict__ logp_out) {
+  constexpr int FO = zh::FO, FI = zh::FI, NW = zh::NW, NS = zh::NS, NL = zh::NL, ZM = zh::BM;
+  __shared__ double sMu[NW * ZM * 4];
+  const int tid = threadIdx.x, l = tid & 63, fr = l & 15, g = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t row0 = (int64_t)blockIdx.x * ZM;
+  const int col0 = 16 * FI * w;
+  const double* ap[FO];
+  const double* bp[FI];
+#pragma unroll
+  for (int t = 0; t < FO; ++t) ap[t] = h1 + min<int64_t>(row0 + 16 * t + fr, N - 1) * H1 + 2 * g;
+#pragma unroll
+  for (int u = 0; u < FI; ++u) bp[u] = W2 + (int64_t)min(col0 + 16 * u + fr, H2 - 1) * H1 + 2 * g;
+  d4 acc[FO][FI];
+#pragma unroll
+  for (int t = 0; t < FO; ++t)
+#pragma unroll
+    for (int u = 0; u < FI; ++u) acc[t][u] = d4{0.0, 0.0, 0.0, 0.0};
+  // stage st reads k = 8 st + 2 g (+1); H1 is even, so a pair is whole or past the end.  The
+  // address is clamped to the last pair and the tail stage's pairs past H1 are zeroed at use.
+  const int nst = (H1 + 7) / 8, nfull = H1 / 8;
+  double2 R[NS][NL];
+  auto load = [&](double2 (&D)[NL], int st) __attribute__((always_inline)) {
+    const int k = min(8 * st, H1 - 2 - 2 * g);  // k + 2 g <= H1 - 2
+#pragma unroll
+    for (int t = 0; t < FO; ++t) D[t] = *reinterpret_cast<const double2*>(ap[t] + k);
+#pragma unroll
+    for (int u = 0; u < FI; ++u) D[FO + u] = *reinterpret_cast<const double2*>(bp[u] + k);
+  };
+  auto mma = [&](const double2 (&D)[NL]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < FO; ++t)
+#pragma unroll
+      for (int u = 0; u < FI; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(D[t].x, D[FO + u].x, acc[t][u], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < FO; ++t)
+#pragma unroll
+      for (int u = 0; u < FI; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(D[t].y, D[FO + u].y, acc[t][u], 0, 0, 0);
+  };
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p) load(R[p], min(p, nst - 1));
+  int st = 0;
+#pragma nounroll
+  for (; st + NS <= nfull; st += NS) {
+#pragma unroll
+    for (int p = 0; p < NS; ++p) {
+      load(R[(p + NS - 1) % NS], min(st + p + NS - 1, nst - 1));
+      mma(R[p]);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < NS; ++p) {
+    if (st + p < nst) {  // uniform
+      if (st + p + NS - 1 < nst) load(R[(p + NS - 1) % NS], st + p + NS - 1);
+      if (st + p >= nfull && 8 * (st + p) + 2 * g >= H1) {  // the tail stage's missing pairs
+#pragma unroll
+        for (int v = 0; v < NL; ++v) R[p][v] = double2{0.0, 0.0};
+      }
+      mma(R[p]);
+    }
+  }
+
+  // ---- epilogue: z2 out, then the head on relu(z2 + b2) (as policy_fwd_kernel's) ----------
+  double b2v[FI];
+#pragma unroll
+  for (int u = 0; u < FI; ++u) {
+    const int c = col0 + 16 * u + fr;
+    b2v[u] = c < H2 ? b2[c] : 0.0;
+#pragma unroll
+    for (int t = 0; t < FO; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t r = row0 + 16 * t + g + 4 * q;
+        if (c < H2 && r < N) z2_out[r * H2 + c] = acc[t][u][q];
+      }
+  }
+  // 4 actions per pass (the fused kernel's 8 would hold 40 more registers next to the 160 of
+  // the accumulators): reduce-scatter over lane bits 8 and 4, sum over bits 2 and 1
+  constexpr int AC = 4;
+  const int er = tid >> 2, ea = tid & 3;  // combine step: row er of the block, action slot ea
+  double lp = 0.0;
+  for (int a0 = 0; a0 < A; a0 += AC) {
+    double wmv[FI][AC];
+#pragma unroll
+    for (int u = 0; u < FI; ++u) {
+      const int c = col0 + 16 * u + fr;
+#pragma unroll
+      for (int a = 0; a < AC; ++a)
+        wmv[u][a] = (c < H2 && a0 + a < A) ? Wm[(int64_t)(a0 + a) * H2 + c] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < FO; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        double p[AC];
+#pragma unroll
+        for (int a = 0; a < AC; ++a) p[a] = 0.0;
+#pragma unroll
+        for (int u = 0; u < FI; ++u) {
+          const double rv = fmax(acc[t][u][q] + b2v[u], 0.0);
+#pragma unroll
+          for (int a = 0; a < AC; ++a) p[a] = fma(rv, wmv[u][a], p[a]);
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          const bool up = (fr & 8) != 0;
+          const double send = up ? p[a] : p[a + 2];
+          p[a] = (up ? p[a + 2] : p[a]) + __shfl_xor(send, 8, kWave);
+        }
+        {
+          const bool up = (fr & 4) != 0;
+          const double send = up ? p[0] : p[1];
+          p[0] = (up ? p[1] : p[0]) + __shfl_xor(send, 4, kWave);
+        }
+        p[0] += __shfl_xor(p[0], 2, kWave);
+        p[0] += __shfl_xor(p[0], 1, kWave);
+        const int comp = ((fr >> 3) & 1) * 2 + ((fr >> 2) & 1);
+        if ((fr & 3) == 0) sMu[(w * ZM + 16 * t + g + 4 * q) * AC + comp] = p[0];
+      }
+    __syncthreads();
+    {
+      const int a = a0 + ea;
+      const int64_t r = row0 + er;
+      double term = 0.0;
+      if (a < A && r < N) {
+        double m = sMu[(0 * ZM + er) * AC + ea];
+#pragma unroll
+        for (int v = 1; v < NW; ++v) m += sMu[(v * ZM + er) * AC + ea];
+        m += bm[a];
+        const double lsa = log_std[a];
+        const double sd = exp(lsa) + kStdEps;
+        const double d = act[r * A + a] - m;
+        mu_out[r * A + a] = m;
+        term = -0.5 * (kLog2Pi + 2.0 * lsa + d * d / (sd * sd));
+      }
+      term += __shfl_xor(term, 2, kWave);
+      term += __shfl_xor(term, 1, kWave);
+      lp += term;
+    }
+    __syncthreads();
+  }
+  if (ea == 0 && row0 + er < N) logp_out[row0 + er] = lp;
+}
+
+template <int FP>
+int launch_split(const double* x, int64_t n, int F, const double* W1, const double* b1, int H1,
+                 const double* W2, const double* b2, int H2, const double* Wm, const double* bm,
+                 const double* log_std, const double* act, int A, double* h1, double* z2,
+                 double* mu, double* logp, uint16_t* mask, hipStream_t st) {
+  const unsigned blocks = (unsigned)((n + 63) / 64);
+  hipLaunchKernelGGL((layer1_kernel<FP>), dim3(blocks), dim3(256), 0, st, x, n, F, W1, b1, H1, h1,
+                     mask);
+  MEPOL_CHECK_LAUNCH();
+  hipLaunchKernelGGL(z2_head_kernel, dim3(blocks), dim3(64 * zh::NW), 0, st, h1, n, H1, W2, b2,
+                     H2, Wm, bm, log_std, act, A, z2, mu, logp);
+  MEPOL_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int FP, bool VEC>
 int launch(const double* x, int64_t n, int F, const double* W1, const double* b1, int H1,
            const double* W2, const double* b2, int H2, const double* Wm, const double* bm,
@@ -338,14 +578,23 @@ static int policy_forward(const double* x, int64_t n, int in_features, const dou
   }
   if (n == 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  // the split form (layer1_kernel + z2_head_kernel) needs 16-B aligned h1 rows; C3 forward
+  // 1.19 ms against the one-kernel form's 1.32 (profiles/r5/f64/forward_split_ab.txt)
+  const bool split = hidden0 % 2 == 0 && ((uintptr_t)h1_out & 15) == 0;
 #define MEPOL_PF(FPV)                                                                        \
+  {                                                                                          \
+  if (split)                                                                                 \
+    return launch_split<FPV>(x, n, in_features, W1, b1, hidden0, W2, b2, hidden1, Wm, bm,     \
+                             log_std, actions, action_dim, h1_out, z2_out, mu_out, logp_out, \
+                             h1_mask_out, st);                                               \
   return (hidden0 % 2 == 0 && hidden0 >= 2)                                                  \
              ? launch<FPV, true>(x, n, in_features, W1, b1, hidden0, W2, b2, hidden1, Wm, bm, \
                                  log_std, actions, action_dim, h1_out, z2_out, mu_out,        \
                                  logp_out, h1_mask_out, st)                                   \
              : launch<FPV, false>(x, n, in_features, W1, b1, hidden0, W2, b2, hidden1, Wm,    \
                                   bm, log_std, actions, action_dim, h1_out, z2_out, mu_out,   \
-                                  logp_out, h1_mask_out, st)
+                                  logp_out, h1_mask_out, st);                                  \
+  }
   if (in_features <= 4) MEPOL_PF(4);
   if (in_features <= 8) MEPOL_PF(8);
   if (in_features <= 16) MEPOL_PF(16);
