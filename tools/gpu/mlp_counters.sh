@@ -14,5 +14,5 @@ for grp in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WA
   i=$((i+1))
   MEPOL_AMD_LIB=$L timeout -s KILL 90 rocprofv3 --pmc $grp -d "$root/$out/pmc$i" -o run -- \
     python3 "$root/tools/mlp_kernels_once.py" > "$root/$out/pmc$i.log" 2>&1 || echo "pass $i failed"
-  (cd "$root" && python3 tools/pmc_table.py "$out/pmc$i/run_results.db" "e" 2>&1 | grep -A1 -E "policy_fwd|dh1_layer1|wgrad_kernel") || true
+  (cd "$root" && python3 tools/pmc_table.py "$out/pmc$i/run_results.db" "e" 2>&1 | grep -A1 -E "policy_fwd|z2_head|layer1_kernel|dh1_layer1|wgrad_kernel") || true
 done
