@@ -87,8 +87,10 @@ def test_predict_matches_forward(cuda):
                                            (100, 5, [37, 45], 3), (65, 1, [16, 320], 32),
                                            (64, 33, [401, 17], 9), (1, 4, [8, 8], 1)])
 def test_policy_forward_kernel_matches_torch(cuda, n, nf, hidden, a):
-    """mepol_policy_forward (csrc/policy_fwd.hip: layer 1 + z2 GEMM + head in one kernel) ==
-    the nn.Linear / ReLU / Gaussian log-density math of src/policy.py:21-51 in torch f64."""
+    """mepol_policy_forward (csrc/policy_fwd.hip) == the nn.Linear / ReLU / Gaussian
+    log-density math of src/policy.py:21-51 in torch f64.  Even h0 runs the split form
+    (layer1_kernel + z2_head_kernel, including the 300-wide K tail); odd h0 (37, 401) the
+    one-kernel form."""
     from mepol_amd import ops
     from mepol_amd import policy as P
 
