@@ -127,10 +127,13 @@ __global__ __launch_bounds__(kNormsThreads) void norms_kernel(const float* __res
   }
 }
 
-// Rejected input (non-finite rows, squared norms beyond f32): norms_kernel counted them into
-// scal[4..5].  The deferred entry point does not stop the stream to look, so every later kernel
-// of the call checks and does nothing (its outputs are then undefined, the caller raises).
-__device__ __forceinline__ bool input_rejected(const unsigned* __restrict__ scal) {
+// The f16 screen does not run for this input: norms_kernel counted into scal[4] the rows with a
+// NaN / inf coordinate (rejected input: the deferred entry point does not stop the stream to
+// look, so every later kernel returns at once, the outputs are undefined and the caller raises)
+// and into scal[5] the finite rows whose squared norm overflows f32 (valid input that the f16
+// scale cannot represent: the screen is skipped and every query takes the exhaustive f64 stage,
+// knn_exact.hip).  Only scal[4] is a rejection.
+__device__ __forceinline__ bool skip_screen(const unsigned* __restrict__ scal) {
   return (scal[4] | scal[5]) != 0u;
 }
 
@@ -149,7 +152,7 @@ __global__ __launch_bounds__(256) void pack16_kernel(const float* __restrict__ X
                                                      float* __restrict__ cpad, int dp) {
   // 4 tiles (kStageRows = 128 candidates) per block of 256 threads, staged through LDS
   extern __shared__ float sx[];
-  if (input_rejected(scal)) return;  // block-uniform, before the barrier
+  if (skip_screen(scal)) return;  // block-uniform, before the barrier
   const int64_t c0 = (int64_t)blockIdx.x * kStageRows;
   const int rows = stage_rows(X, n, d, c0, sx);
   // cpad rows of this block: one contiguous span, written with dwordx4 in order
@@ -254,7 +257,7 @@ __global__ __launch_bounds__(256) void refine_kernel(
   const int64_t xcd = bx & 7, per = nb >> 3, rem = nb & 7;
   const int64_t qb = xcd * per + min(xcd, rem) + (bx >> 3);
   const int64_t q = qb * 4 + w;
-  if (q >= nq || input_rejected(cmax_bits)) return;
+  if (q >= nq || skip_screen(cmax_bits)) return;
   // Candidate entries of this query: 2*split ascending partial lists of list_len each, the last
   // slot of each carrying that lane's prune bound (select16_kernel).
   const float* lv = lists_v + q * M;
@@ -610,12 +613,14 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   return 0;
 }
 
-// MEPOL_KNN_SEED=0: every candidate range starts its prune bound at +inf.  The certified
-// output is the same bits either way (tests/test_gpu_knn.py::test_knn_seed_invariance); only
-// the partial lists, and so the count of queries sent to the exhaustive stage, differ.
+// Prune-bound seeds of the selection: 2 (default) = the probe sample's bound (probe16_kernel)
+// and the bounds finished candidate ranges publish; MEPOL_KNN_SEED=1: the published bounds only
+// (round 5); 0: every candidate range starts its prune bound at +inf.  The certified output is
+// the same bits either way (tests/test_gpu_knn.py::test_knn_seed_invariance); only the partial
+// lists, and so the count of queries sent to the exhaustive stage, differ.
 static int select_seed() {
   const char* e = getenv("MEPOL_KNN_SEED");
-  return (e && e[0] == '0') ? 0 : 1;
+  return (e && (e[0] == '0' || e[0] == '1')) ? e[0] - '0' : 2;
 }
 
 // refine_kernel's merge of the partial lists: per-list binary-search ranks (2); the kernel
@@ -731,6 +736,22 @@ static int knn_impl(const float* cand, int64_t n_cand, const float* query, int64
       set_error("mepol_knn: Input contains NaN or infinity (%u rows)", bad[0]);
       return kErrBadArg;
     }
+    if (bad[1] && wide_buffer_bytes(P.nq, 1, P.kp1) == 0) {
+      // Every query goes to the exhaustive stage: take its fast form over the whole grid (the
+      // transposed candidates, in the padded-row area the screen would have used: nc * dp >=
+      // nc * d floats) instead of the queued-query form the screen's fallback uses.
+      ea.candT = (float*)(ws + P.off_cpad);
+      launch_transpose_validate(cand, P.nc, P.d, (float*)ea.candT, nullptr, st);
+      ea.all = 1;
+      ea.scal = nullptr;
+      ea.wbuf_d = nullptr;
+      ea.wbuf_i = nullptr;
+      if (n_fallback_out)
+        MEPOL_HIP(hipMemsetD32Async((hipDeviceptr_t)n_fallback_out, (int)P.nq, 1, st));
+      launch_exact_stage(ea, st);
+      MEPOL_CHECK_LAUNCH();
+      return 0;
+    }
   }
   if (P.exhaustive) {
     ea.all = 1;
@@ -753,12 +774,16 @@ static int knn_impl(const float* cand, int64_t n_cand, const float* query, int64
   MEPOL_CHECK_LAUNCH();
   {
     int* seed = nullptr;
-    if (P.split > 1 && select_seed()) {
+    const int seeding = select_seed();
+    if (seeding == 2 || (seeding == 1 && P.split > 1)) {
       seed = (int*)(ws + P.off_seed);
-      MEPOL_HIP(hipMemsetD32Async((hipDeviceptr_t)seed, kSeedNone, (size_t)P.nq, st));
+      // the probe kernel writes every query's seed; without it ranges start from +inf
+      if (seeding == 1)
+        MEPOL_HIP(hipMemsetD32Async((hipDeviceptr_t)seed, kSeedNone, (size_t)P.nq, st));
     }
-    const SelectArgs sa{ap16,        query,  P.nq,   P.d,    P.nct, P.split, P.tiles_per_split,
-                        P.keep,      P.LIST16, P.nh, P.nqt,  cmax,  lv,      li, seed};
+    const SelectArgs sa{ap16,   query,    P.nq, P.d,   P.nct, P.split, P.tiles_per_split,
+                        P.keep, P.LIST16, P.nh, P.nqt, cmax,  lv,      li,
+                        seed,   seeding == 2};
     switch (P.KS16) {
       case 1: launch_select<1>(sa, st); break;
       case 2: launch_select<2>(sa, st); break;

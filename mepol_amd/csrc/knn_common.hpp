@@ -93,6 +93,7 @@ struct SelectArgs {
   float* out_v;
   int* out_i;
   int* seed;  // [nq] ordered keys of the per-query prune bounds the ranges publish (nullable)
+  int probe;  // seed from the probe sample first (probe16_kernel; needs seed)
 };
 
 // Order-preserving map of a float to an int (atomicMin on the int orders like the float; the

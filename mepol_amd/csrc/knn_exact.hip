@@ -459,7 +459,7 @@ __global__ __launch_bounds__(256) void transpose_validate_kernel(const float* __
   if (tid == 0) {
     unsigned c = 0;
     for (int i = 0; i < kTrRows; ++i) c += rowbad[i];
-    if (c) atomicAdd(bad, c);
+    if (c && bad) atomicAdd(bad, c);
   }
 }
 

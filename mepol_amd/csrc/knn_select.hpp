@@ -65,6 +65,29 @@ __device__ __forceinline__ void flush_groups(float (&ld)[LIST], int (&li)[LIST],
   }
 }
 
+// B operands (queries) of lane l's query column: B[k = 16 s + 8h + j][col = l&31] = sigma q_f
+// (f < d), 1 (f == d), 0, split into f16 hi + lo.  Unconditional loads at clamped addresses (a
+// load under a per-element condition makes hipcc wait for each one in turn).
+template <int KS16>
+__device__ __forceinline__ void query_frags(const float* __restrict__ query, int64_t q, int64_t nq,
+                                            int d, float sg, int h, f16x8 (&bhi)[KS16],
+                                            f16x8 (&blo)[KS16]) {
+  const bool qvalid = q < nq;
+  const float* qrow = query + min(q, nq - 1) * d;
+#pragma unroll
+  for (int s = 0; s < KS16; ++s)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int f = 16 * s + 8 * h + j;
+      const float x = qrow[min(f, d - 1)];  // finite (validated): x * 0 = 0
+      const float v = ((f < d ? sg : 0.f) * x + (f == d ? 1.f : 0.f)) * (qvalid ? 1.f : 0.f);
+      _Float16 a, b;
+      split_f16(v, a, b);
+      bhi[s][j] = a;
+      blo[s][j] = b;
+    }
+}
+
 // Partial top-LIST lists of every query over its split's tile range.  The queries are split into
 // f16 hi + lo (2^-22 relative).  NH = 1 (candidate-hi, the default): the candidates are the f16
 // hi halves of A and 2 MFMAs per k-step (A_hi q_hi + A_hi q_lo) accumulate in f32; the value's
@@ -108,27 +131,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   const float inv_s2 = 1.f / (sg * sg);  // exact: sigma is a power of two
   constexpr bool kQueryLo = NH == 2 || KS16 >= 4;  // make_plan's bound covers the rest
 
-  // B operands (queries): B[k = 16 s + 8h + j][col = l&31] = sigma q_f (f<d), 1 (f==d), 0.
-  // Unconditional loads at clamped addresses (a load under a per-element condition makes hipcc
-  // wait for each one in turn).
   f16x8 bhi[KS16], blo[KS16];
   const int64_t q = qt0 * 32 + (l & 31);
   const bool qvalid = q < nq;
-  {
-    const float* qrow = query + min(q, nq - 1) * d;
-#pragma unroll
-    for (int s = 0; s < KS16; ++s)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int f = 16 * s + 8 * h + j;
-        const float x = qrow[min(f, d - 1)];  // finite (validated): x * 0 = 0
-        const float v = ((f < d ? sg : 0.f) * x + (f == d ? 1.f : 0.f)) * (qvalid ? 1.f : 0.f);
-        _Float16 a, b;
-        split_f16(v, a, b);
-        bhi[s][j] = a;
-        blo[s][j] = b;
-      }
-  }
+  query_frags<KS16>(query, q, nq, d, sg, h, bhi, blo);
 
   LaneList<LIST> S;
 #pragma unroll
@@ -261,6 +267,91 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// Probe seeds (round 6).  Before the selection, every query's prune bound is seeded from a
+// strided sample of kProbeTiles candidate tiles spread over the whole candidate set: per lane
+// the kProbeKth-th smallest of its per-tile minima (each minimum is a distinct candidate's
+// approximate value, so at least kProbeKth candidates lie at or below it), the smaller of the
+// two lanes of the query goes to seed[q].  Without it the first candidate range of every query
+// starts from +inf and pays the whole list warm-up, ~LIST ln(n / LIST) insertions per lane,
+// the bulk of the select's list work; from the probe seed a range inserts only the candidates
+// below the sample's quantile.  Any seed is sound (select16_kernel's seed comment); this one
+// leaves ~8 / (32 kProbeTiles) of all candidates below it, far more than k + 1, so the lists
+// still certify.
+// ---------------------------------------------------------------------------------------
+constexpr int kProbeTiles = 128;
+constexpr int kProbeKth = 8;
+
+template <int KS16, int NH>
+__global__ __launch_bounds__(256) void probe16_kernel(const _Float16* __restrict__ apack,
+                                                      const float* __restrict__ query, int64_t nq,
+                                                      int d, int64_t nct,
+                                                      const unsigned* __restrict__ scal,
+                                                      int* __restrict__ seed) {
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int l = threadIdx.x & 63;
+  const int64_t qt0 = (int64_t)blockIdx.x * 4 + w;
+  if (qt0 * 32 >= nq || (scal[4] | scal[5])) return;  // wave-uniform
+  const int h = l >> 5;
+  const float sg = knn_scale(scal);
+  constexpr bool kQueryLo = NH == 2 || KS16 >= 4;
+  f16x8 bhi[KS16], blo[KS16];
+  const int64_t q = qt0 * 32 + (l & 31);
+  query_frags<KS16>(query, q, nq, d, sg, h, bhi, blo);
+  constexpr int NV = NH * KS16;
+  const f32x4* abase = reinterpret_cast<const f32x4*>(apack) + l;
+  const int64_t np = min<int64_t>(kProbeTiles, nct);
+  const int64_t stride = nct / np;  // >= 1
+  float kth[kProbeKth];
+#pragma unroll
+  for (int j = 0; j < kProbeKth; ++j) kth[j] = INFINITY;
+  constexpr int U = 4;  // tiles in flight
+#pragma nounroll
+  for (int64_t i0 = 0; i0 < np; i0 += U) {
+    f32x4 A[U][NV];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t t = min(i0 + u, np - 1) * stride + stride / 2;
+#pragma unroll
+      for (int v = 0; v < NV; ++v) A[u][v] = abase[(t * NV + v) * 64];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f32x16 acc = {};
+#pragma unroll
+      for (int s = 0; s < KS16; ++s) {
+        const f16x8 ah = __builtin_bit_cast(f16x8, A[u][NH * s]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, bhi[s], acc, 0, 0, 0);
+        if constexpr (kQueryLo)
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, blo[s], acc, 0, 0, 0);
+        if constexpr (NH == 2) {
+          const f16x8 al = __builtin_bit_cast(f16x8, A[u][2 * s + 1]);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, bhi[s], acc, 0, 0, 0);
+        }
+      }
+      float m = acc[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) m = fminf(m, acc[r]);
+      // the tile repeated by a clamped index (np % U) must not count twice
+      if (i0 + u >= np) m = INFINITY;
+      // branch-free insert into the ascending kth list
+#pragma unroll
+      for (int j = kProbeKth - 1; j >= 1; --j)
+        kth[j] = m < kth[j - 1] ? kth[j - 1] : fminf(kth[j], m);
+      kth[0] = fminf(kth[0], m);
+    }
+  }
+  const float v = fminf(kth[kProbeKth - 1], __shfl_xor(kth[kProbeKth - 1], 32, kWave));
+  if (q < nq && h == 0) seed[q] = float_order_key(v);
+}
+
+template <int KS16, int NH>
+static void launch_probe16(const SelectArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((probe16_kernel<KS16, NH>), dim3((unsigned)((a.nqt + 3) / 4)), dim3(256), 0,
+                     st, a.apack, a.query, a.nq, a.d, a.nct, a.scal, a.seed);
+}
+
 // ---------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------
@@ -290,6 +381,12 @@ static void launch_select16_ks(const SelectArgs& a, hipStream_t st) {
 
 template <int KS16>
 void launch_select(const SelectArgs& a, hipStream_t st) {
+  if (a.seed && a.probe) {
+    if (a.nh == 2)
+      launch_probe16<KS16, 2>(a, st);
+    else
+      launch_probe16<KS16, 1>(a, st);
+  }
   if (a.nh == 2)
     launch_select16_ks<KS16, 2>(a, st);
   else

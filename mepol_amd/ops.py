@@ -5,6 +5,7 @@ must live on a ROCm device; dtypes follow the reference (f64 values, int64 indic
 API boundary; int32 indices internally).
 """
 import math
+import threading
 
 import torch
 
@@ -103,14 +104,10 @@ class KnnInputCheck:
     # its slot until raise_if_invalid() has read it (or it is collected); with every slot held
     # a new one is allocated, so no check can read another call's counts.
     _free = []
-    _lock = None
+    _lock = threading.Lock()
 
     def __init__(self, invalid_dev):
-        import threading
-
         cls = KnnInputCheck
-        if cls._lock is None:
-            cls._lock = threading.Lock()
         with cls._lock:
             slot = cls._free.pop() if cls._free else None
         self._host = slot if slot is not None else torch.empty(2, dtype=torch.int32,
@@ -130,7 +127,14 @@ class KnnInputCheck:
         if self._host is not None:
             self._event.synchronize()
             self._nonfinite = int(self._host[0])
+            overflow = int(self._host[1])
             self._release()
+            if overflow and not self._nonfinite:
+                import warnings
+
+                warnings.warn(f"mepol_knn: {overflow} rows have a squared norm beyond f32; the f16 "
+                              "screen was skipped and every query took the exhaustive f64 scan "
+                              "(correct, but far slower than the screen)")
         if self._nonfinite:
             raise MepolInputError(f"mepol_knn failed (rc=1001): mepol_knn: Input contains NaN or "
                                   f"infinity ({self._nonfinite} rows)")
@@ -144,8 +148,14 @@ class KnnInputCheck:
                 KnnInputCheck._free.append(host)
 
     def __del__(self):
+        # never block in a finalizer (it runs wherever garbage collection does, and at
+        # interpreter shutdown): return the slot only if its copy has already landed, else
+        # drop it (the pinned block is freed with the tensor)
         try:
-            self._release()
+            host, self._host = getattr(self, "_host", None), None
+            if host is not None and self._event.query():
+                with KnnInputCheck._lock:
+                    KnnInputCheck._free.append(host)
         except Exception:
             pass
 

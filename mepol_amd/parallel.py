@@ -106,20 +106,22 @@ class ShardedEpoch:
     # -- per-epoch setup ------------------------------------------------------------------------
     def build_knn(self):
         cand = self._gather(self.next_states).reshape(self.N, -1)
-        self.D, self.I, self.idx32T, check = self.ops.knn(cand, self.k + 1,
-                                                          query=self.next_states,
-                                                          defer_check=True)
-        idx_all = self._gather(self.idx32T[: self.k].contiguous())       # [G, k, n_local]
+        D, I, idx32T, check = self.ops.knn(cand, self.k + 1, query=self.next_states,
+                                           defer_check=True)
+        idx_all = self._gather(idx32T[: self.k].contiguous())       # [G, k, n_local]
         idx_allT = idx_all.permute(1, 0, 2).reshape(self.k, self.N).contiguous()
-        self.csr = self.ops.csr_build(idx_allT, self.k, self.n_local, col_offset=self.R0,
-                                      row_offset=0, nq=self.N)
+        csr = self.ops.csr_build(idx_allT, self.k, self.n_local, col_offset=self.R0,
+                                 row_offset=0, nq=self.N)
         # The input check is read only now, with the gather and the CSR build queued behind
         # the k-NN (one host wait less in the epoch set-up).  A rejected input (a NaN / inf
         # coordinate) is rejected on every rank alike -- the check covers the gathered
         # candidates, which every rank holds -- so all ranks issued the same gather and all
         # raise here; the k-NN kernels returned early, the gathered rows are undefined and the
-        # CSR build (which bounds-checks its ids) is discarded with them.
+        # CSR build (which bounds-checks its ids) is discarded with them.  The epoch's
+        # attributes are assigned only after the check passed: a caller that catches the error
+        # never sees undefined neighbour tables.
         check.raise_if_invalid()
+        self.D, self.I, self.idx32T, self.csr = D, I, idx32T, csr
         return self.D, self.I
 
     # -- policy log-probs -----------------------------------------------------------------------
