@@ -486,9 +486,15 @@ def run(args):
             "tools/knn_probe.py at this shape, run by this bench before it touched the GPU; "
             "FETCH_SIZE x2 (gfx950)")
         line["roofline"]["traffic_per_kernel"] = traffic_kernels
-        line["roofline"]["traffic_compulsory"] = 4 * d * (nq + N) + 8 * (k + 1) * nq
+        comp = 4 * d * (nq + N) + 8 * (k + 1) * nq
+        line["roofline"]["traffic_compulsory"] = comp
+        line["roofline"]["traffic_over_compulsory"] = round(traffic / comp, 2)
     elif traffic:
         line["roofline"]["traffic_source"] = os.path.relpath(pmc_path, ROOT)
+    if traffic:
+        # BASELINE's literal metric ("k-NN HBM GB/s, % of 8 TB/s"): the measured HBM bytes per
+        # call over the call's time.  The candidates stay in L2 / MALL, so this is far from the
+        # bound the call runs against (roofline.bound: the f16 MFMA peak)
         gbps = traffic / (knn_ms * 1e-3) / 1e9
         line["roofline"]["hbm_GBps"] = round(gbps, 1)
         line["roofline"]["hbm_frac"] = round(gbps / PEAK_HBM_GBPS, 4)

@@ -352,6 +352,7 @@ static void launch_probe16(const SelectArgs& a, hipStream_t st) {
                      st, a.apack, a.query, a.nq, a.d, a.nct, a.scal, a.seed);
 }
 
+
 // ---------------------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------------------

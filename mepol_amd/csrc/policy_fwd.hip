@@ -307,57 +307,76 @@ __global__ __launch_bounds__(kThreads) void policy_fwd_kernel(
 // ---------------------------------------------------------------------------------------
 // Split form (hidden0 even): layer 1 alone, then z2 + head with no LDS operand staging.
 // ---------------------------------------------------------------------------------------
-// h1 = relu(x W1^T + b1) and its bit mask, one wave per 16 rows: the row's x fragment stays in
-// registers (k = 4 s + g), the 16-column tiles of W1 stream from L2, stores are whole 128-B
-// row segments.  HBM-write bound (h1 is N x h0 f64).
-template <int FP>
+// h1 = relu(x W1^T + b1) and its bit mask, one wave per RG groups of 16 rows: the rows' x
+// fragments stay in registers (k = 4 s + g), the 16-column tiles of W1 stream from L2 with the
+// next tile's fragment loaded under the current tile's MFMAs (RG independent accumulation chains
+// of NS steps), stores are whole 128-B row segments.  HBM-write bound (h1 is N x h0 f64).
+// Round 6: RG = 2 (was one row group per wave and no prefetch: every wave re-read all of W1
+// through L1 per 16 rows, 1.3 GB per call at C3, and waited for each tile).
+template <int FP, int RG>
 __global__ __launch_bounds__(256) void layer1_kernel(const double* __restrict__ x, int64_t N,
                                                      int F, const double* __restrict__ W1,
                                                      const double* __restrict__ b1, int H1,
                                                      double* __restrict__ h1_out,
                                                      uint16_t* __restrict__ mask_out) {
-  constexpr int NS = FP / 4, NCH = NS < 4 ? NS : 4;
+  constexpr int NS = FP / 4;
   const int l = threadIdx.x & 63, fr = l & 15, g = l >> 4;
-  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 16 * RG;
   if (r0 >= N) return;  // wave-uniform
-  double xv[NS];
-  const int64_t xr = min<int64_t>(r0 + fr, N - 1);
+  double xv[RG][NS];
 #pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    const int f = 4 * s + g;
-    const double v = x[xr * F + min(f, F - 1)];
-    xv[s] = f < F ? v : 0.0;
+  for (int rg = 0; rg < RG; ++rg) {
+    const int64_t xr = min<int64_t>(r0 + 16 * rg + fr, N - 1);
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      const int f = 4 * s + g;
+      const double v = x[xr * F + min(f, F - 1)];
+      xv[rg][s] = f < F ? v : 0.0;
+    }
   }
   const int nkt = (H1 + 15) / 16, mw = nkt;
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int c = kt * 16 + fr;
-    const double* wr = W1 + (int64_t)min(c, H1 - 1) * F;
-    double wv[NS];
+  double wv[2][NS], bc[2];
+  auto loadw = [&](int b, int kt) __attribute__((always_inline)) {
+    const int c = min(kt * 16 + fr, H1 - 1);
+    const double* wr = W1 + (int64_t)c * F;
 #pragma unroll
     for (int s = 0; s < NS; ++s) {
       const int f = 4 * s + g;
       const double v = wr[min(f, F - 1)];
-      wv[s] = f < F ? v : 0.0;
+      wv[b][s] = f < F ? v : 0.0;
     }
-    const double bc = b1[min(c, H1 - 1)];
-    d4 hc[NCH];
+    bc[b] = b1[c];
+  };
+  auto tile = [&](int b, int kt) __attribute__((always_inline)) {
+    if (kt + 1 < nkt) loadw(b ^ 1, kt + 1);  // uniform
+    d4 h[RG];
 #pragma unroll
-    for (int u = 0; u < NCH; ++u) hc[u] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int rg = 0; rg < RG; ++rg) h[rg] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int s = 0; s < NS; ++s)
-      hc[s % NCH] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[s], wv[s], hc[s % NCH], 0, 0, 0);
-    d4 h = hc[0];
 #pragma unroll
-    for (int u = 1; u < NCH; ++u) h += hc[u];
+      for (int rg = 0; rg < RG; ++rg)
+        h[rg] = __builtin_amdgcn_mfma_f64_16x16x4f64(xv[rg][s], wv[b][s], h[rg], 0, 0, 0);
+    const int c = kt * 16 + fr;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t r = r0 + g + 4 * q;
-      const double v = c < H1 ? fmax(h[q] + bc, 0.0) : 0.0;
-      if (c < H1 && r < N) h1_out[r * H1 + c] = v;
-      const uint64_t bits = __ballot(v > 0.0);
-      if (mask_out && fr == 0 && r < N) mask_out[r * mw + kt] = (uint16_t)(bits >> (16 * g));
-    }
+    for (int rg = 0; rg < RG; ++rg)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t r = r0 + 16 * rg + g + 4 * q;
+        const double v = c < H1 ? fmax(h[rg][q] + bc[b], 0.0) : 0.0;
+        if (c < H1 && r < N) h1_out[r * H1 + c] = v;
+        const uint64_t bits = __ballot(v > 0.0);
+        if (mask_out && fr == 0 && r < N) mask_out[r * mw + kt] = (uint16_t)(bits >> (16 * g));
+      }
+  };
+  loadw(0, 0);
+  int kt = 0;
+#pragma nounroll
+  for (; kt + 1 < nkt; kt += 2) {
+    tile(0, kt);
+    tile(1, kt + 1);
   }
+  if (kt < nkt) tile(0, kt);
 }
 
 // z2 = h1 W2^T and the head, one workgroup per 64-row block: wave w owns columns
@@ -523,14 +542,20 @@ __global__ __launch_bounds__(64 * zh::NW) __attribute__((amdgpu_waves_per_eu(2))
   if (ea == 0 && row0 + er < N) logp_out[row0 + er] = lp;
 }
 
+#ifndef MEPOL_L1_RG
+#define MEPOL_L1_RG 2
+#endif
+constexpr int kLayer1RowGroups = MEPOL_L1_RG;  // row groups of 16 per wave (layer1_kernel)
+
 template <int FP>
 int launch_split(const double* x, int64_t n, int F, const double* W1, const double* b1, int H1,
                  const double* W2, const double* b2, int H2, const double* Wm, const double* bm,
                  const double* log_std, const double* act, int A, double* h1, double* z2,
                  double* mu, double* logp, uint16_t* mask, hipStream_t st) {
   const unsigned blocks = (unsigned)((n + 63) / 64);
-  hipLaunchKernelGGL((layer1_kernel<FP>), dim3(blocks), dim3(256), 0, st, x, n, F, W1, b1, H1, h1,
-                     mask);
+  constexpr int RG = kLayer1RowGroups;
+  hipLaunchKernelGGL((layer1_kernel<FP, RG>), dim3((unsigned)((n + 64 * RG - 1) / (64 * RG))),
+                     dim3(256), 0, st, x, n, F, W1, b1, H1, h1, mask);
   MEPOL_CHECK_LAUNCH();
   hipLaunchKernelGGL(z2_head_kernel, dim3(blocks), dim3(64 * zh::NW), 0, st, h1, n, H1, W2, b2,
                      H2, Wm, bm, log_std, act, A, z2, mu, logp);
