@@ -239,7 +239,7 @@ __global__ __launch_bounds__(256) void refine_kernel(
     const int* __restrict__ lists_i, const unsigned* __restrict__ cmax_bits, int e_terms,
     double* __restrict__ Dout,
     int64_t* __restrict__ I64, int32_t* __restrict__ I32, int* __restrict__ flag_count,
-    int* __restrict__ flag_list, int rank_merge) {
+    int* __restrict__ flag_list, double* __restrict__ flag_bound, int rank_merge) {
   __shared__ int sel[4][64];
   __shared__ float selv[4][64];  // rank merge: approximate value of sel[r]
   constexpr int kRM = MAXP <= 4 ? MAXP : 1;  // rank merge for M <= 256 entries
@@ -446,6 +446,8 @@ __global__ __launch_bounds__(256) void refine_kernel(
   if (!ok && l == 0) {
     const int slot = atomicAdd(flag_count, 1);
     flag_list[slot] = (int)q;
+    // the (k+1)-th smallest exact d^2 evaluated here bounds the answer's (exact stage)
+    flag_bound[slot] = eki != INT_MAX ? ek : INFINITY;
   }
 }
 
@@ -463,7 +465,7 @@ struct Plan {
   int M;          // refine input entries per query: 2*split*LIST16
   int64_t nc, nq, nct, nqt, tiles_per_split;
   bool exhaustive;  // no f16 screen: every query scanned exactly (knn_exact.hip block select)
-  size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_part, off_cpad, off_seed;
+  size_t off_apack, off_scalars, off_lv, off_li, off_flag, off_fbound, off_part, off_cpad, off_seed;
   size_t off_candT, off_wbuf, total;
 };
 
@@ -601,6 +603,8 @@ static int make_plan(int64_t nc, int64_t nq, int d, int kp1, int split_hint, Pla
   off = align_up(off + nl * sizeof(int), 256);
   P->off_flag = off;
   off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(int), 256);
+  P->off_fbound = off;  // refine's bound per queued query (exact stage)
+  off = align_up(off + (size_t)std::max<int64_t>(nq, 1) * sizeof(double), 256);
   P->off_part = off;  // exact fallback: kExactGrid partial lists of <= 64 (f64, int32)
   off = align_up(off + (size_t)kExactGrid * 64 * (sizeof(double) + sizeof(int)), 256);
   P->dp = (d + 31) / 32 * 32;
@@ -629,13 +633,13 @@ constexpr int kRankMerge = 2;
 
 static void launch_refine(const Plan& P, const float* cpad, const float* query, const float* lv,
                           const int* li, const unsigned* cmax, double* D, int64_t* I64,
-                          int32_t* I32, int* fc, int* fl, hipStream_t st) {
+                          int32_t* I32, int* fc, int* fl, double* fb, hipStream_t st) {
   dim3 g((unsigned)((P.nq + 3) / 4));
   // MAXP = ceil(M / 64) <= 32
 #define MEPOL_REFINE(MP)                                                                          \
   hipLaunchKernelGGL((refine_kernel<kRefineList, MP>), g, dim3(256), 0, st, cpad, P.dp, P.nc,     \
                      query, P.nq, P.d, P.kp1, P.M, P.LIST16, lv, li, cmax, P.e_terms, D, I64,     \
-                     I32, fc, fl, kRankMerge)
+                     I32, fc, fl, fb, kRankMerge)
   if (P.maxp <= 2)
     MEPOL_REFINE(2);
   else if (P.maxp <= 4)
@@ -774,7 +778,17 @@ static int knn_impl(const float* cand, int64_t n_cand, const float* query, int64
   MEPOL_CHECK_LAUNCH();
   {
     int* seed = nullptr;
-    const int seeding = select_seed();
+    int seeding = select_seed();
+    // The probe seed leaves ~kProbeKth * nc / (32 np) candidates below it (the smaller of the two
+    // lanes' kProbeKth-th tile minima over np sampled tiles); it pays only where that is far
+    // above k + 1.  Split-candidate plans (low-dimensional, duplicate-heavy data: GridWorld,
+    // MountainCar) keep the published bounds only: exact ties at a tight seed would cost
+    // certification (measured: C2S k-NN 1.5 -> 10.9 ms with the probe).
+    if (seeding == 2) {
+      const double np = (double)std::min<int64_t>(kProbeTiles, P.nct);
+      const double below = kProbeKth * (double)P.nc / (32.0 * np);
+      if (P.nh != 1 || below < 4.0 * P.kp1) seeding = 1;
+    }
     if (seeding == 2 || (seeding == 1 && P.split > 1)) {
       seed = (int*)(ws + P.off_seed);
       // the probe kernel writes every query's seed; without it ranges start from +inf
@@ -793,10 +807,13 @@ static int knn_impl(const float* cand, int64_t n_cand, const float* query, int64
   }
   MEPOL_CHECK_LAUNCH();
   int* flist = (int*)(ws + P.off_flag);
-  launch_refine(P, cpad, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, st);
+  double* fbound = (double*)(ws + P.off_fbound);
+  launch_refine(P, cpad, query, lv, li, cmax, dist_out, idx_out, idx32_out, fcount, flist, fbound,
+                st);
   MEPOL_CHECK_LAUNCH();
   // 4. queued queries (or all of them, scal[5]) by the exhaustive stage
   ea.flag_list = flist;
+  ea.flag_bound = fbound;
   ea.part_d = (double*)(ws + P.off_part);
   ea.part_i = (int*)(ws + P.off_part + (size_t)kExactGrid * 64 * sizeof(double));
   launch_exact_stage(ea, st);

@@ -74,6 +74,11 @@ __device__ __forceinline__ void split_f16(float v, _Float16& hi, _Float16& lo) {
   lo = (_Float16)(v - (float)hi);  // v - hi is exact in f32
 }
 
+// probe seeds (knn_select.hpp, probe16_kernel): sampled candidate tiles per query, and which
+// smallest tile minimum of a lane becomes the seed
+constexpr int kProbeTiles = 256;
+constexpr int kProbeKth = 8;
+
 constexpr float kPadNorm16 = 60000.f;  // scaled |c|^2 of padding candidates (> any real D')
 
 // Arguments of the selection launch (make_plan's fields the select kernels read).
@@ -185,6 +190,9 @@ struct ExactArgs {
   int* part_i;
   double* wbuf_d;         // block-select form, lists beyond LDS: grid x cap entries (nullable)
   int* wbuf_i;
+  // per queued query (flag_list order): an upper bound on its (k+1)-th exact squared distance,
+  // the (k+1)-th smallest exact d^2 refine evaluated (nullable; unused when every query runs)
+  const double* flag_bound;
 };
 
 // Block-select capacity (entries) for kp1: room for kp1 plus one step of every thread.

@@ -40,10 +40,12 @@ __device__ __forceinline__ void stage_report(const ExactArgs& a) {
 // Exhaustive f64 top-kp1 of query xq over candidates [c0, c1), lexicographic (dist, idx):
 // per-thread sorted lists, then kp1 rounds of block argmin; round r's winner goes to
 // emit(r, d, i) on thread 0 (i = INT_MAX, d = inf when the range holds fewer than kp1).
+// ub: only candidates with d^2 <= ub can be among the first kp1 (refine's bound for a queued
+// query, +inf otherwise): the others are never inserted.
 template <int LIST, typename Emit>
 __device__ __forceinline__ void exact_scan(const float* __restrict__ cand, int64_t c0, int64_t c1,
                                            const float* __restrict__ xq, int d, int kp1,
-                                           double* red_d, int* red_i, Emit emit) {
+                                           double ub, double* red_d, int* red_i, Emit emit) {
   const int tid = threadIdx.x;
   const int l = tid & 63, w = tid >> 6;
   double ld[LIST];
@@ -57,7 +59,7 @@ __device__ __forceinline__ void exact_scan(const float* __restrict__ cand, int64
   for (int64_t c = c0 + tid; c < c1; c += blockDim.x) {
     const double x = exact_d2(xq, cand + c * d, d);
     const int xi = (int)c;
-    if (lex_less(x, xi, ld[LIST - 1], li[LIST - 1])) {
+    if (x <= ub && lex_less(x, xi, ld[LIST - 1], li[LIST - 1])) {
       bool cc[LIST];
 #pragma unroll
       for (int j = 0; j < LIST; ++j) cc[j] = lex_less(x, xi, ld[j], li[j]);
@@ -118,6 +120,22 @@ __host__ __device__ inline int exact_nchunk(int count, int grid) {
   return (count <= 0 || count >= grid) ? 1 : grid / count;
 }
 
+// Refine's bound for queued query fi (round 6): its candidates beyond the (k+1)-th exact d^2 that
+// refine evaluated cannot be among the first k+1, so the scan inserts almost only the answer
+// (C2S, ~600-1300 queued queries on dense d = 2 data: the per-thread list insertions were the
+// stage's cost).  The relative slack only admits more candidates; the answer is the same.
+__device__ __forceinline__ double stage_bound(const ExactArgs& a, int fi) {
+  if (!a.flag_bound || a.all || (a.scal && a.scal[5])) return INFINITY;
+  const double b = a.flag_bound[fi];
+  return b * (1.0 + 0x1p-40);
+}
+
+// block select of one query (defined with the block-select form below)
+constexpr int kExactLdsCap = 2048;  // exact_kernel's block-select buffer: kp1 <= 64, cap - step
+template <bool kTransposed>
+__device__ void wide_query(const ExactArgs& a, int64_t q, double ub, double* bd, int* bi, int cap,
+                           int* s_cnt);
+
 template <int LIST>
 __global__ __launch_bounds__(256) void exact_kernel(ExactArgs a) {
   __shared__ double red_d[4];
@@ -126,9 +144,20 @@ __global__ __launch_bounds__(256) void exact_kernel(ExactArgs a) {
   stage_report(a);
   const int nchunk = a.part_d ? exact_nchunk(count, (int)gridDim.x) : 1;
   if (nchunk == 1) {
+    __shared__ double s_bd[kExactLdsCap];
+    __shared__ int s_bi[kExactLdsCap];
+    __shared__ int s_cnt;
     for (int fi = blockIdx.x; fi < count; fi += gridDim.x) {
       const int64_t q = stage_query(a, fi);
-      exact_scan<LIST>(a.cand, 0, a.nc, a.query + q * a.d, a.d, a.kp1, red_d, red_i,
+      const double ub = stage_bound(a, fi);
+      if (ub < INFINITY) {  // block-uniform
+        // refine's bound leaves ~k+1 candidates: append them to LDS and sort them once instead
+        // of per-thread lists and k+1 block argmin rounds (C2S: 500-1300 queued queries)
+        wide_query<false>(a, q, ub, s_bd, s_bi, kExactLdsCap, &s_cnt);
+        continue;
+      }
+      exact_scan<LIST>(a.cand, 0, a.nc, a.query + q * a.d, a.d, a.kp1, stage_bound(a, fi), red_d,
+                       red_i,
                        [&](int r, double bd, int bi) {
                          a.D[q * a.kp1 + r] = sqrt_rn(bd);
                          if (a.I64) a.I64[q * a.kp1 + r] = bi;
@@ -142,7 +171,8 @@ __global__ __launch_bounds__(256) void exact_kernel(ExactArgs a) {
   const int64_t q = stage_query(a, fi);
   const int64_t c0 = a.nc * ch / nchunk, c1 = a.nc * (ch + 1) / nchunk;
   const int64_t o = ((int64_t)fi * nchunk + ch) * a.kp1;
-  exact_scan<LIST>(a.cand, c0, c1, a.query + q * a.d, a.d, a.kp1, red_d, red_i,
+  exact_scan<LIST>(a.cand, c0, c1, a.query + q * a.d, a.d, a.kp1, stage_bound(a, fi), red_d,
+                   red_i,
                    [&](int r, double bd, int bi) {
                      a.part_d[o + r] = bd;
                      a.part_i[o + r] = bi;
@@ -281,6 +311,91 @@ __device__ __forceinline__ void block_sort(double* bd, int* bi, int n, int P) {
   }
 }
 
+// Block select of one query: the block appends every candidate below the running kp1-th
+// (distance, index) -- from ub on, refine's bound for a queued query, +inf otherwise -- to bd/bi
+// (cap entries, LDS or global), compacts to the first kp1 by a bitonic sort when the buffer
+// fills, and writes the first kp1.  Every thread of the block calls it.
+template <bool kTransposed>
+__device__ void wide_query(const ExactArgs& a, int64_t q, double ub, double* bd, int* bi, int cap,
+                           int* s_cnt) {
+  const int tid = threadIdx.x;
+  const int d = a.d, kp1 = a.kp1;
+  const int64_t nc = a.nc;
+  const float* __restrict__ qrow = a.query + q * d;
+  if (tid == 0) *s_cnt = 0;
+  __syncthreads();
+  double thr_d = ub;  // the running kp1-th (distance, index), block-uniform
+  int thr_i = INT_MAX;
+  for (int64_t c0 = 0; c0 < nc; c0 += kWideStep) {
+    double s[kWideUnroll];
+    int64_t cl[kWideUnroll];
+#pragma unroll
+    for (int u = 0; u < kWideUnroll; ++u) {
+      s[u] = 0.0;
+      cl[u] = min(c0 + u * kWideThreads + tid, nc - 1);  // clamped: loads stay in bounds
+    }
+#pragma unroll 2
+    for (int f = 0; f < d; ++f) {
+      const double qf = (double)qrow[f];
+      float x[kWideUnroll];
+#pragma unroll
+      for (int u = 0; u < kWideUnroll; ++u)
+        x[u] = kTransposed ? a.candT[(int64_t)f * nc + cl[u]] : a.cand[cl[u] * d + f];
+#pragma unroll
+      for (int u = 0; u < kWideUnroll; ++u) {
+        const double t = __dsub_rn(qf, (double)x[u]);
+        s[u] = __dadd_rn(s[u], __dmul_rn(t, t));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kWideUnroll; ++u) {
+      const int64_t c = c0 + u * kWideThreads + tid;
+      const bool pass = c < nc && lex_less(s[u], (int)c, thr_d, thr_i);
+      const unsigned long long m = __ballot(pass);
+      if (m) {  // one LDS atomic per wave: slots by prefix count of the ballot
+        int base = 0;
+        if ((tid & 63) == __builtin_ctzll(m)) base = atomicAdd(s_cnt, __popcll(m));
+        base = __shfl(base, __builtin_ctzll(m), kWave);
+        if (pass) {
+          const int slot =
+              base + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+          bd[slot] = s[u];
+          bi[slot] = (int)c;
+        }
+      }
+    }
+    __syncthreads();
+    const int n = *s_cnt;
+    // every wave has read the count before any wave appends the next step's candidates
+    // (a late read would see them and could disagree on the compaction below)
+    __syncthreads();
+    if (n > cap - kWideStep) {  // block-uniform: keep the first kp1, tighten the threshold
+      int P = 1;
+      while (P < n) P <<= 1;
+      block_sort(bd, bi, n, P);
+      const int keep = min(n, kp1);
+      if (keep == kp1) {
+        thr_d = bd[kp1 - 1];
+        thr_i = bi[kp1 - 1];
+      }
+      __syncthreads();  // every thread has read the threshold before s_cnt changes
+      if (tid == 0) *s_cnt = keep;
+      __syncthreads();
+    }
+  }
+  const int n = *s_cnt;
+  int P = 1;
+  while (P < n) P <<= 1;
+  block_sort(bd, bi, n, P);
+  for (int r = tid; r < kp1; r += kWideThreads) {
+    a.D[q * kp1 + r] = sqrt_rn(bd[r]);
+    if (a.I64) a.I64[q * kp1 + r] = bi[r];
+    if (a.I32) a.I32[(int64_t)r * a.nq + q] = bi[r];  // transposed [kp1][nq]
+  }
+  __syncthreads();  // the buffer is reused by the next query
+}
+
 template <bool kTransposed, bool kGlobalBuf>
 __global__ __launch_bounds__(kWideThreads) void wide_exact_kernel(ExactArgs a, int cap) {
   extern __shared__ char wide_smem[];
@@ -296,85 +411,8 @@ __global__ __launch_bounds__(kWideThreads) void wide_exact_kernel(ExactArgs a, i
   }
   const int count = stage_count(a);
   stage_report(a);
-  const int tid = threadIdx.x;
-  const int d = a.d, kp1 = a.kp1;
-  const int64_t nc = a.nc;
-  for (int fi = blockIdx.x; fi < count; fi += gridDim.x) {
-    const int64_t q = stage_query(a, fi);
-    const float* __restrict__ qrow = a.query + q * d;
-    if (tid == 0) s_cnt = 0;
-    __syncthreads();
-    double thr_d = INFINITY;  // the running kp1-th (distance, index), block-uniform
-    int thr_i = INT_MAX;
-    for (int64_t c0 = 0; c0 < nc; c0 += kWideStep) {
-      double s[kWideUnroll];
-      int64_t cl[kWideUnroll];
-#pragma unroll
-      for (int u = 0; u < kWideUnroll; ++u) {
-        s[u] = 0.0;
-        cl[u] = min(c0 + u * kWideThreads + tid, nc - 1);  // clamped: loads stay in bounds
-      }
-#pragma unroll 2
-      for (int f = 0; f < d; ++f) {
-        const double qf = (double)qrow[f];
-        float x[kWideUnroll];
-#pragma unroll
-        for (int u = 0; u < kWideUnroll; ++u)
-          x[u] = kTransposed ? a.candT[(int64_t)f * nc + cl[u]] : a.cand[cl[u] * d + f];
-#pragma unroll
-        for (int u = 0; u < kWideUnroll; ++u) {
-          const double t = __dsub_rn(qf, (double)x[u]);
-          s[u] = __dadd_rn(s[u], __dmul_rn(t, t));
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kWideUnroll; ++u) {
-        const int64_t c = c0 + u * kWideThreads + tid;
-        const bool pass = c < nc && lex_less(s[u], (int)c, thr_d, thr_i);
-        const unsigned long long m = __ballot(pass);
-        if (m) {  // one LDS atomic per wave: slots by prefix count of the ballot
-          int base = 0;
-          if ((tid & 63) == __builtin_ctzll(m)) base = atomicAdd(&s_cnt, __popcll(m));
-          base = __shfl(base, __builtin_ctzll(m), kWave);
-          if (pass) {
-            const int slot =
-                base + __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32),
-                                                 __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-            bd[slot] = s[u];
-            bi[slot] = (int)c;
-          }
-        }
-      }
-      __syncthreads();
-      const int n = s_cnt;
-      // every wave has read the count before any wave appends the next step's candidates
-      // (a late read would see them and could disagree on the compaction below)
-      __syncthreads();
-      if (n > cap - kWideStep) {  // block-uniform: keep the first kp1, tighten the threshold
-        int P = 1;
-        while (P < n) P <<= 1;
-        block_sort(bd, bi, n, P);
-        const int keep = min(n, kp1);
-        if (keep == kp1) {
-          thr_d = bd[kp1 - 1];
-          thr_i = bi[kp1 - 1];
-        }
-        __syncthreads();  // every thread has read the threshold before s_cnt changes
-        if (tid == 0) s_cnt = keep;
-        __syncthreads();
-      }
-    }
-    const int n = s_cnt;
-    int P = 1;
-    while (P < n) P <<= 1;
-    block_sort(bd, bi, n, P);
-    for (int r = tid; r < kp1; r += kWideThreads) {
-      a.D[q * kp1 + r] = sqrt_rn(bd[r]);
-      if (a.I64) a.I64[q * kp1 + r] = bi[r];
-      if (a.I32) a.I32[(int64_t)r * a.nq + q] = bi[r];  // transposed [kp1][nq]
-    }
-    __syncthreads();  // the buffer is reused by the next query
-  }
+  for (int fi = blockIdx.x; fi < count; fi += gridDim.x)
+    wide_query<kTransposed>(a, stage_query(a, fi), stage_bound(a, fi), bd, bi, cap, &s_cnt);
 }
 
 template <int LIST>

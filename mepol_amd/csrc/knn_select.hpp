@@ -280,8 +280,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) void
 // leaves ~8 / (32 kProbeTiles) of all candidates below it, far more than k + 1, so the lists
 // still certify.
 // ---------------------------------------------------------------------------------------
-constexpr int kProbeTiles = 128;
-constexpr int kProbeKth = 8;
 
 template <int KS16, int NH>
 __global__ __launch_bounds__(256) void probe16_kernel(const _Float16* __restrict__ apack,
