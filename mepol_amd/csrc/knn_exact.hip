@@ -109,6 +109,11 @@ __device__ __forceinline__ void exact_scan(const float* __restrict__ cand, int64
       li[LIST - 1] = INT_MAX;
     }
     if (tid == 0) emit(r, bd, bi);
+    if (bi == INT_MAX) {  // block-uniform: every list is empty, the rest are +inf too
+      if (tid == 0)
+        for (int rr = r + 1; rr < kp1; ++rr) emit(rr, (double)INFINITY, INT_MAX);
+      break;
+    }
   }
 }
 
@@ -130,7 +135,8 @@ __device__ __forceinline__ double stage_bound(const ExactArgs& a, int fi) {
   return b * (1.0 + 0x1p-40);
 }
 
-// block select of one query (defined with the block-select form below)
+// bitonic sort and block select of one query (defined with the block-select form below)
+__device__ void block_sort(double* bd, int* bi, int n, int P);
 constexpr int kExactLdsCap = 2048;  // exact_kernel's block-select buffer: kp1 <= 64, cap - step
 template <bool kTransposed>
 __device__ void wide_query(const ExactArgs& a, int64_t q, double ub, double* bd, int* bi, int cap,
@@ -193,6 +199,39 @@ __global__ __launch_bounds__(256) void exact_merge_kernel(ExactArgs a, int grid)
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
   const int64_t q = stage_query(a, fi);
   const int64_t base = (int64_t)fi * nchunk * kp1;
+  if (stage_bound(a, fi) < INFINITY) {  // block-uniform
+    // The chunks kept only candidates within refine's bound (a few times k+1 in all): gather
+    // the finite entries of the partial lists and sort them once (k+1 rounds of block argmin
+    // over 512 list heads took ~58 us for the one queued query of a C3 call).
+    __shared__ double s_bd[kExactLdsCap];
+    __shared__ int s_bi[kExactLdsCap];
+    __shared__ int s_n;
+    if (tid == 0) s_n = 0;
+    __syncthreads();
+    for (int e = tid; e < nchunk * kp1; e += 256) {
+      const double x = a.part_d[base + e];
+      if (x < INFINITY) {
+        const int slot = atomicAdd(&s_n, 1);
+        if (slot < kExactLdsCap) {
+          s_bd[slot] = x;
+          s_bi[slot] = a.part_i[base + e];
+        }
+      }
+    }
+    __syncthreads();
+    const int n = s_n;
+    if (n <= kExactLdsCap) {  // block-uniform; else the argmin rounds below
+      int P = 1;
+      while (P < n || P < kp1) P <<= 1;
+      block_sort(s_bd, s_bi, n, P);  // (distance, index): the same order as the rounds
+      for (int r = tid; r < kp1; r += 256) {
+        a.D[q * kp1 + r] = sqrt_rn(s_bd[r]);
+        if (a.I64) a.I64[q * kp1 + r] = s_bi[r];
+        if (a.I32) a.I32[(int64_t)r * a.nq + q] = s_bi[r];  // transposed [kp1][nq]
+      }
+      return;
+    }
+  }
   constexpr int kPer = 2;  // lists per thread: nchunk <= grid <= 512
   int pos[kPer] = {0, 0};
   for (int r = 0; r < kp1; ++r) {
@@ -284,7 +323,7 @@ size_t wide_buffer_bytes(int64_t nq, int all, int kp1) {
 
 // Bitonic sort of bd/bi[0, P) ascending by (distance, index), P a power of two; entries
 // [n, P) are padding.  Every thread of the block calls it.
-__device__ __forceinline__ void block_sort(double* bd, int* bi, int n, int P) {
+__device__ void block_sort(double* bd, int* bi, int n, int P) {
   const int tid = threadIdx.x;
   for (int i = n + tid; i < P; i += kWideThreads) {
     bd[i] = INFINITY;
