@@ -244,3 +244,12 @@ def test_knn_seed_invariance(cuda, monkeypatch):
         assert np.array_equal(D1, D0) and np.array_equal(I1, I0)
         Do, Io = O.knn_exact(X, kp1)
         assert np.array_equal(D1, Do) and np.array_equal(I1, Io)
+    # probe-seeded plans (one k-step half, >= 4 (k + 1) candidates expected below the probe's
+    # bound): the probed (2) and published-only (1) seeds certify the same bits
+    Xp = rng.standard_normal((9000, 8)).astype(np.float32)
+    Xp[1::7] = Xp[::7][: len(Xp[1::7])]  # exact duplicates: ties at the seed
+    Do, Io = O.knn_exact(Xp, 2)
+    for mode in ("2", "1"):
+        monkeypatch.setenv("MEPOL_KNN_SEED", mode)
+        D, I, _, _ = _knn(Xp, 2)
+        assert np.array_equal(D, Do) and np.array_equal(I, Io), mode

@@ -10,12 +10,12 @@ if [ "$2" = tests ]; then
     tests/test_gpu_knn.py tests/test_gpu_knn_total.py > "$out/tests.log" 2>&1
   rc=$?; tail -3 "$out/tests.log"; [ $rc = 0 ] || exit $rc
 fi
-for sd in 2 1; do
+for sd in ${SEEDS:-2 1}; do
   MEPOL_KNN_SEED=$sd timeout -k 10 120 python3 tools/knn_probe.py --reps 4 $CFG > "$out/seed$sd.log" 2>&1 || exit 1
   echo "seed $sd: $(grep 'knn ms' $out/seed$sd.log)"
 done
 cd /tmp && export TMPDIR=/tmp
-for sd in 2 1; do
+for sd in ${SEEDS:-2 1}; do
   MEPOL_KNN_SEED=$sd timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$root/$out/prof$sd" -o run -- \
     python3 "$root/tools/knn_probe.py" --reps 3 $CFG > "$root/$out/prof$sd.log" 2>&1 || exit 1
   echo "== seed $sd"
