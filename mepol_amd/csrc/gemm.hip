@@ -5,11 +5,15 @@
 //
 // Tiling: a workgroup owns a BM x BN tile of C (WR x WC waves, each FR x FC 16x16 fragments,
 // accumulators in registers), streams K through LDS in k-tiles of 16 (double-buffered, one
-// barrier per tile).  Rows of both operand tiles are stored with a 144-B stride (16 + 2
-// doubles): a fragment read is a ds_read_b128 whose 16 lanes of a row group hit all 64 banks
-// once.  The k order inside a tile is permuted so that each lane's four k-steps are contiguous
-// (lane group g = lane>>4 feeds k = 4g + s at step s for both operands), i.e. two b128 reads
-// give a lane all of its fragment data for the tile.
+// barrier per tile).  The k order inside a tile is permuted so that each lane's four k-steps
+// are contiguous (lane group g = lane>>4 feeds k = 4g + s at step s for both operands), i.e.
+// two b128 reads give a lane all of its fragment data for the tile.  Rows of both operand
+// tiles are 128 B (two to a 256-B bank row) with the 16-B slots XOR-swizzled per row
+// (lds_slot): a ds_read_b128 is serviced in the lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31} (+32), i.e. rows fr 0-3, 12-15 of one k-slot with rows 4-11 of the next
+// one, and the swizzle puts each group's 16 reads on 16 distinct slots (the round-5 144-B
+// padded stride left two of them 2-way: SQ_LDS_BANK_CONFLICT 3.3e7 per C3 dh1 call); the
+// stores (8-lane groups, one row) stay conflict-free.
 #include "common.hpp"
 
 #include <type_traits>
@@ -18,7 +22,15 @@ namespace mepol {
 namespace gemm {
 
 constexpr int KT = 16;  // k per LDS tile
-constexpr int KP = 18;  // padded LDS row (doubles)
+constexpr int KP = 16;  // LDS row (doubles), swizzled by lds_slot
+
+// physical 16-B slot of logical slot c (k = 2c, 2c + 1 of the tile) in LDS row r: c ^ h(r) with
+// h(r) in {0, 1, 4, 5} from bits 1 and 3 of r.  Read group {rows 0-3, 12-15 at slot j, rows
+// 4-11 at j + 2}: h over rows {0, 2, 12, 14} (and the odd ones) is {0, 1, 4, 5}, over rows
+// {4, 6, 8, 10} the same set, so j ^ h and (j + 2) ^ h never meet (bit 1 differs).
+__device__ __forceinline__ int lds_slot(int r, int c) {
+  return c ^ (((r >> 1) & 1) | (((r >> 3) & 1) << 2));
+}
 typedef double d4 __attribute__((ext_vector_type(4)));
 
 // XCD-aware tile order for a 1-D grid: workgroup L runs on XCD L % 8, so consecutive tiles
@@ -79,7 +91,7 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
       const int ch = tid + p * T, r = ch >> 3, k = kb + 2 * (ch & 7);
       if (ch < P::CA) {
         const bool ok = row0 + r < N && k < K;
-        *reinterpret_cast<double2*>(sA + (buf * BM + r) * KP + 2 * (ch & 7)) =
+        *reinterpret_cast<double2*>(sA + (buf * BM + r) * KP + 2 * lds_slot(r, ch & 7)) =
             ok ? ra[p] : double2{0.0, 0.0};
       }
     }
@@ -88,7 +100,7 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
       const int ch = tid + p * T, r = ch >> 3, k = kb + 2 * (ch & 7);
       if (ch < P::CB) {
         const bool ok = col0 + r < M && k < K;
-        *reinterpret_cast<double2*>(sB + (buf * BN + r) * KP + 2 * (ch & 7)) =
+        *reinterpret_cast<double2*>(sB + (buf * BN + r) * KP + 2 * lds_slot(r, ch & 7)) =
             ok ? rb[p] : double2{0.0, 0.0};
       }
     }
@@ -100,6 +112,8 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
     for (int j = 0; j < FC; ++j) acc[i][j] = d4{0.0, 0.0, 0.0, 0.0};
 
   const int fr = lane & 15, g = lane >> 4;
+  // a lane's two slots in its fragment rows (every fragment row is fr mod 16: same swizzle)
+  const int sl0 = 2 * lds_slot(fr, 2 * g), sl1 = 2 * lds_slot(fr, 2 * g + 1);
   gload(0);
   lstore(0, 0);
   __syncthreads();
@@ -109,15 +123,15 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
     double2 a[FR][2], b[FC][2];
 #pragma unroll
     for (int i = 0; i < FR; ++i) {
-      const double* p = sA + (buf * BM + wr * FR * 16 + i * 16 + fr) * KP + 4 * g;
-      a[i][0] = *reinterpret_cast<const double2*>(p);
-      a[i][1] = *reinterpret_cast<const double2*>(p + 2);
+      const double* p = sA + (buf * BM + wr * FR * 16 + i * 16 + fr) * KP;
+      a[i][0] = *reinterpret_cast<const double2*>(p + sl0);
+      a[i][1] = *reinterpret_cast<const double2*>(p + sl1);
     }
 #pragma unroll
     for (int j = 0; j < FC; ++j) {
-      const double* p = sB + (buf * BN + wc * FC * 16 + j * 16 + fr) * KP + 4 * g;
-      b[j][0] = *reinterpret_cast<const double2*>(p);
-      b[j][1] = *reinterpret_cast<const double2*>(p + 2);
+      const double* p = sB + (buf * BN + wc * FC * 16 + j * 16 + fr) * KP;
+      b[j][0] = *reinterpret_cast<const double2*>(p + sl0);
+      b[j][1] = *reinterpret_cast<const double2*>(p + sl1);
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
