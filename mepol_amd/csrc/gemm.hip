@@ -54,7 +54,9 @@ struct Cfg {
 // fragment j]^T over all of K for the workgroup tile (row0, col0).  Operand loads read clamped
 // (always valid) addresses; out-of-range values are zeroed when the registers are written to
 // LDS, after the MFMA block, so no select waits on a load right after issuing it.
-template <int WR, int WC, int FR, int FC>
+// DEEP: two register sets, the global loads of tile t + 2 issued while tile t is computed (the
+// store of tile t + 1 then waits on loads a whole tile older); 24 more VGPRs.
+template <int WR, int WC, int FR, int FC, bool DEEP = false>
 __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int64_t N, int K,
                                               int64_t lda, const double* __restrict__ B, int M,
                                               int64_t ldb, int64_t row0, int col0, double* lds,
@@ -68,8 +70,9 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
   const int nkt = (K + KT - 1) / KT;
   const int k2 = K - 2;  // last 16-B aligned pair start (K even)
 
-  double2 ra[P::PA], rb[P::PB];
-  auto gload = [&](int kt) __attribute__((always_inline)) {
+  using RA = double2[P::PA];
+  using RB = double2[P::PB];
+  auto gload = [&](int kt, RA& ra, RB& rb) __attribute__((always_inline)) {
     const int kb = kt * KT;
 #pragma unroll
     for (int p = 0; p < P::PA; ++p) {
@@ -84,7 +87,7 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
                                                 min(k, k2));
     }
   };
-  auto lstore = [&](int kt, int buf) __attribute__((always_inline)) {
+  auto lstore = [&](int kt, int buf, const RA& ra, const RB& rb) __attribute__((always_inline)) {
     const int kb = kt * KT;
 #pragma unroll
     for (int p = 0; p < P::PA; ++p) {
@@ -114,12 +117,7 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
   const int fr = lane & 15, g = lane >> 4;
   // a lane's two slots in its fragment rows (every fragment row is fr mod 16: same swizzle)
   const int sl0 = 2 * lds_slot(fr, 2 * g), sl1 = 2 * lds_slot(fr, 2 * g + 1);
-  gload(0);
-  lstore(0, 0);
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nkt) gload(kt + 1);
+  auto compute = [&](int buf) __attribute__((always_inline)) {
     double2 a[FR][2], b[FC][2];
 #pragma unroll
     for (int i = 0; i < FR; ++i) {
@@ -145,8 +143,39 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
         }
       }
     }
-    if (kt + 1 < nkt) lstore(kt + 1, buf ^ 1);
+  };
+
+  RA ra0, ra1;
+  RB rb0, rb1;
+  gload(0, ra0, rb0);
+  lstore(0, 0, ra0, rb0);
+  if constexpr (DEEP) {
+    if (nkt > 1) gload(1, ra1, rb1);
     __syncthreads();
+    int kt = 0;
+    for (; kt + 1 < nkt; kt += 2) {  // tile kt in buffer 0, kt + 1 in buffer 1
+      if (kt + 2 < nkt) gload(kt + 2, ra0, rb0);
+      compute(0);
+      lstore(kt + 1, 1, ra1, rb1);
+      __syncthreads();
+      if (kt + 3 < nkt) gload(kt + 3, ra1, rb1);
+      compute(1);
+      if (kt + 2 < nkt) lstore(kt + 2, 0, ra0, rb0);
+      __syncthreads();
+    }
+    if (kt < nkt) {
+      compute(0);
+      __syncthreads();
+    }
+  } else {
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nkt) gload(kt + 1, ra0, rb0);
+      compute(buf);
+      if (kt + 1 < nkt) lstore(kt + 1, buf ^ 1, ra0, rb0);
+      __syncthreads();
+    }
   }
 }
 
@@ -220,7 +249,7 @@ __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
   const int64_t row0 = (int64_t)rb * BM;
   const int col0 = (tile % ncb) * BN;
   d4 acc[FR][FC];
-  gemm_mainloop<WR, WC, FR, FC>(dz2, N, K, K, W2t, M, K, row0, col0, lds, acc);
+  gemm_mainloop<WR, WC, FR, FC, true>(dz2, N, K, K, W2t, M, K, row0, col0, lds, acc);
 
   // Every epilogue operand in ONE batch of unconditional loads (clamped addresses) before the
   // first use: the ReLU mask of h1 at the wave's accumulator elements and the [x | 1] operands.
