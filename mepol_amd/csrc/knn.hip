@@ -232,8 +232,38 @@ __device__ __forceinline__ double exact_d2_pad(const float* __restrict__ a,
   return s;
 }
 
+// exact_d2_pad with the first 32 coordinates of a already in registers (qa[u] = a[min(u, d - 1)]):
+// the same operations in the same order.
+__device__ __forceinline__ double exact_d2_pad_pre(const float (&qa)[32],
+                                                   const float* __restrict__ a,
+                                                   const float* __restrict__ b, int d) {
+  constexpr int kCh = 32;
+  double s = 0.0;
+  for (int f0 = 0; f0 < d; f0 += kCh) {
+    float av[kCh];
+    f32x4 bv[kCh / 4];
+#pragma unroll
+    for (int u = 0; u < kCh / 4; ++u) bv[u] = reinterpret_cast<const f32x4*>(b + f0)[u];
+    if (f0 == 0) {
+#pragma unroll
+      for (int u = 0; u < kCh; ++u) av[u] = qa[u];
+    } else {
+#pragma unroll
+      for (int u = 0; u < kCh; ++u) av[u] = a[min(f0 + u, d - 1)];
+    }
+#pragma unroll
+    for (int u = 0; u < kCh; ++u) {
+      if (f0 + u < d) {  // uniform condition
+        const double t = __dsub_rn((double)av[u], (double)bv[u >> 2][u & 3]);
+        s = __dadd_rn(s, __dmul_rn(t, t));
+      }
+    }
+  }
+  return s;
+}
+
 template <int LIST, int MAXP>
-__global__ __launch_bounds__(256) void refine_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void refine_kernel(
     const float* __restrict__ cpad, int dp, int64_t nc, const float* __restrict__ query,
     int64_t nq, int d, int kp1, int M, int list_len, const float* __restrict__ lists_v,
     const int* __restrict__ lists_i, const unsigned* __restrict__ cmax_bits, int e_terms,
@@ -258,6 +288,15 @@ __global__ __launch_bounds__(256) void refine_kernel(
   const int64_t qb = xcd * per + min(xcd, rem) + (bx >> 3);
   const int64_t q = qb * 4 + w;
   if (q >= nq || skip_screen(cmax_bits)) return;
+  // The query row first: |q|^2 and the exact distances' first 32 coordinates are then loaded
+  // beside the lists instead of after the merge (the wave fences below keep memory operations
+  // from moving across them)
+  const float* xq = query + q * d;
+  float qa[32];
+#pragma unroll
+  for (int u = 0; u < 32; ++u) qa[u] = xq[min(u, d - 1)];
+  double qn2 = 0.0;
+  for (int f = l; f < d; f += 64) qn2 += (double)xq[f] * (double)xq[f];
   // Candidate entries of this query: 2*split ascending partial lists of list_len each, the last
   // slot of each carrying that lane's prune bound (select16_kernel).
   const float* lv = lists_v + q * M;
@@ -307,7 +346,8 @@ __global__ __launch_bounds__(256) void refine_kernel(
       // smaller index -- O(lists x log LIST16) LDS reads per entry instead of all M.
       const int nl = mtot / list_len;
       const float2* se = sent[w];
-#pragma nounroll
+      // unrolled: the lists' binary searches are independent LDS read chains
+#pragma unroll 4
       for (int s = 0; s < nl; ++s) {
         const float2* L = se + s * list_len;
 #pragma unroll
@@ -379,9 +419,6 @@ __global__ __launch_bounds__(256) void refine_kernel(
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 
   // |q|^2 and the selection's error bound E (certification below; any summation order)
-  const float* xq = query + q * d;
-  double qn2 = 0.0;
-  for (int f = l; f < d; f += 64) qn2 += (double)xq[f] * (double)xq[f];
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) qn2 += __shfl_xor(qn2, m, kWave);
   const double cmax = (double)__uint_as_float(*cmax_bits);
@@ -410,7 +447,7 @@ __global__ __launch_bounds__(256) void refine_kernel(
   if (l < mcut) {
     const int c = sel[w][l];
     if (c >= 0) {
-      dd = exact_d2_pad(xq, cpad + (int64_t)c * dp, d);
+      dd = exact_d2_pad_pre(qa, xq, cpad + (int64_t)c * dp, d);
       di = c;
     }
   }
