@@ -1,5 +1,6 @@
 """Time ops.policy_forward at the C3 policy shape (N=200k, 29->[400,300]->8, f64) for
-rocprofv3 kernel stats (layer1_kernel / z2_head_kernel).  Usage: python tools/l1_probe.py [reps]"""
+rocprofv3 kernel stats (layer1_kernel / z2_head_kernel).  Usage: python tools/l1_probe.py [reps]
+(L1_N=rows overrides N, e.g. 25000 for the per-rank share of an 8-GPU run)"""
 import os
 import sys
 
@@ -10,7 +11,7 @@ from mepol_amd import ops  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 f64 = dict(dtype=torch.float64, device="cuda")
-n, nf, h0, h1w, a = 200000, 29, 400, 300, 8
+n, nf, h0, h1w, a = int(os.environ.get("L1_N", 200000)), 29, 400, 300, 8
 torch.manual_seed(0)
 x = torch.randn(n, nf, **f64)
 W1, b1 = torch.randn(h0, nf, **f64) * 0.2, torch.randn(h0, **f64) * 0.1
