@@ -315,11 +315,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
     float v = INFINITY;
     int ix = INT_MAX;
     if (e < nval) {
-      const int ii = lix[e];
-      if (ii >= 0 && ii < nc) {
-        v = lv[e];
-        ix = ii;
-      }
+      // both loads issued before either is tested (a value load behind the index test would
+      // wait out a second memory round trip)
+      const int ii = __builtin_nontemporal_load(lix + e);
+      const float vv = __builtin_nontemporal_load(lv + e);
+      const bool ok = ii >= 0 && ii < nc;
+      v = ok ? vv : INFINITY;
+      ix = ok ? ii : INT_MAX;
     }
     ev[p] = v;
     ei[p] = ix;
