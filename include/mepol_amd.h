@@ -35,7 +35,7 @@ extern "C" {
 /* Bumped on every incompatible change of the signatures below (2: mepol_rollout_mlp takes a
  * workspace; mepol_gemm_dpp removed; 3: mepol_iw_normalize_gathered takes the per-rank
  * trajectory sums).  mepol_abi_version() returns the library's value. */
-#define MEPOL_ABI_VERSION 3
+#define MEPOL_ABI_VERSION 4
 
 #define MEPOL_ERR_BAD_ARG 1001
 #define MEPOL_ERR_WORKSPACE 1002
@@ -197,6 +197,16 @@ int mepol_head_backward(const double* grad_logp, const double* z, int64_t n, int
                         const double* act, const double* mu, int a_dim, double* dz, double* dWm,
                         double* dbm, double* dlog_std, double* dbz, void* workspace,
                         size_t workspace_bytes, void* stream);
+/* mepol_head_backward in two launches on possibly different streams: phase 1 = the row kernel
+ * (dz and the per-block records in the workspace), phase 2 = the fixed-order reduces of those
+ * records into dWm, dbm, dlog_std, dbz (the caller orders phase 2 after phase 1 and keeps the
+ * workspace until phase 2 ran).  Same arguments and the same bits as mepol_head_backward
+ * (ABI 4; the off-policy iteration runs phase 2 beside the dW2 / dh1 GEMMs). */
+int mepol_head_backward_phase(const double* grad_logp, const double* z, int64_t n, int hidden,
+                              const double* bz, const double* Wm, const double* log_std,
+                              const double* act, const double* mu, int a_dim, double* dz,
+                              double* dWm, double* dbm, double* dlog_std, double* dbz,
+                              void* workspace, size_t workspace_bytes, int phase, void* stream);
 /* Input layer h = relu(x W^T + b): x [n, in] (in <= 64), W [out, in], b [out], h [n, out];
  * backward from dh = dL/dh and h: dW [out, in], db [out] (nullable). */
 int mepol_layer_forward(const double* x, int64_t n, int in_features, const double* W,

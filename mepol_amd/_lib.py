@@ -16,7 +16,7 @@ _c_dbl = ctypes.c_double
 _c_sz = ctypes.c_size_t
 _c_vp = ctypes.c_void_p
 
-ABI_VERSION = 3  # include/mepol_amd.h MEPOL_ABI_VERSION
+ABI_VERSION = 4  # include/mepol_amd.h MEPOL_ABI_VERSION
 
 # name -> argtypes (restype is int unless listed in _RESTYPES)
 SIGNATURES = {
@@ -52,6 +52,9 @@ SIGNATURES = {
     "mepol_head_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
     "mepol_head_backward": [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_int,
                             _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
+    "mepol_head_backward_phase": [_c_vp, _c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                  _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_sz, _c_int,
+                                  _c_vp],
     "mepol_weight_grad_workspace_size": [_c_i64, _c_int, _c_int, ctypes.POINTER(_c_sz)],
     "mepol_weight_grad": [_c_vp, _c_i64, _c_int, _c_vp, _c_int, _c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_layer_forward": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp],

@@ -562,11 +562,14 @@ extern "C" int mepol_head_workspace_size(int64_t n, int hidden, int a_dim, size_
 
 // dz [n, hidden] (nullable: skip the input gradient), dWm [a_dim, hidden], dbm [a_dim],
 // dlog_std [a_dim] are written (not accumulated).
-extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int64_t n, int hidden,
-                                   const double* bz, const double* Wm, const double* log_std,
-                                   const double* act, const double* mu, int a_dim, double* dz,
-                                   double* dWm, double* dbm, double* dlog_std, double* dbz,
-                                   void* workspace, size_t workspace_bytes, void* stream) {
+// phase 0: the whole backward; 1: the row kernel only (its per-block records into the
+// workspace, and dz); 2: the two fixed-order reduces of those records only (dWm, dbm,
+// dlog_std, dbz), e.g. on another stream ordered after phase 1.
+static int head_backward(const double* grad_logp, const double* z, int64_t n, int hidden,
+                         const double* bz, const double* Wm, const double* log_std,
+                         const double* act, const double* mu, int a_dim, double* dz, double* dWm,
+                         double* dbm, double* dlog_std, double* dbz, void* workspace,
+                         size_t workspace_bytes, int phase, void* stream) {
   if (n <= 0 || hidden <= 0 || hidden > 64 * kMaxCols || a_dim <= 0 || a_dim > kMaxA ||
       !grad_logp || !z || !Wm || !log_std || !act || !mu || !dWm || !dbm || !dlog_std ||
       !workspace) {
@@ -582,6 +585,8 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
   }
   hipStream_t st = (hipStream_t)stream;
   double* pdW = (double*)workspace;
+  const int64_t m = (int64_t)a_dim * hidden + 2 * a_dim + hidden;
+  if (phase == 2) return reduce_records(pdW, nb, m, a_dim * hidden, a_dim, dWm, dbm, dlog_std, dbz, st);
   if (a_dim > 8) {
     const int apw = a_dim <= 12 ? 12 : a_dim <= 16 ? 16 : a_dim <= 20 ? 20 : a_dim <= 24 ? 24 : 32;
     const int hs = (hidden + 63) / 64 * 64;  // block width: one column per lane
@@ -601,7 +606,7 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
     MEPOL_HEAD_BWDW(32)
 #undef MEPOL_HEAD_BWDW
     MEPOL_CHECK_LAUNCH();
-    const int64_t m = (int64_t)a_dim * hidden + 2 * a_dim + hidden;
+    if (phase == 1) return 0;
     return reduce_records(pdW, nb, m, a_dim * hidden, a_dim, dWm, dbm, dlog_std, dbz, st);
   }
   const int nc = (hidden + 63) / 64;
@@ -618,6 +623,30 @@ extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int
 #undef MEPOL_HEAD_BWD_A
 #undef MEPOL_HEAD_BWD
   MEPOL_CHECK_LAUNCH();
-  const int64_t m = (int64_t)a_dim * hidden + 2 * a_dim + hidden;
+  if (phase == 1) return 0;
   return reduce_records(pdW, nb, m, a_dim * hidden, a_dim, dWm, dbm, dlog_std, dbz, st);
+}
+
+extern "C" int mepol_head_backward(const double* grad_logp, const double* z, int64_t n, int hidden,
+                                   const double* bz, const double* Wm, const double* log_std,
+                                   const double* act, const double* mu, int a_dim, double* dz,
+                                   double* dWm, double* dbm, double* dlog_std, double* dbz,
+                                   void* workspace, size_t workspace_bytes, void* stream) {
+  return head_backward(grad_logp, z, n, hidden, bz, Wm, log_std, act, mu, a_dim, dz, dWm, dbm,
+                       dlog_std, dbz, workspace, workspace_bytes, 0, stream);
+}
+
+extern "C" int mepol_head_backward_phase(const double* grad_logp, const double* z, int64_t n,
+                                         int hidden, const double* bz, const double* Wm,
+                                         const double* log_std, const double* act,
+                                         const double* mu, int a_dim, double* dz, double* dWm,
+                                         double* dbm, double* dlog_std, double* dbz,
+                                         void* workspace, size_t workspace_bytes, int phase,
+                                         void* stream) {
+  if (phase != 1 && phase != 2) {
+    set_error("mepol_head_backward_phase: phase must be 1 (row kernel) or 2 (reduces)");
+    return kErrBadArg;
+  }
+  return head_backward(grad_logp, z, n, hidden, bz, Wm, log_std, act, mu, a_dim, dz, dWm, dbm,
+                       dlog_std, dbz, workspace, workspace_bytes, phase, stream);
 }

@@ -345,10 +345,16 @@ def head_forward(z, Wm, bm, log_std, act, bz=None, mu_out=None, logp_out=None):
 
 
 def head_backward(grad_logp, z, Wm, log_std, act, mu, bz=None, need_dz=True, ws=None,
-                  outs=None):
+                  outs=None, reduce_stream=None, defer_reduce=False):
     """Returns (dz or None, dWm, dbm, dlog_std, dbz or None).  `ws`: caller-owned scratch
     (head_workspace); default: the per-stream eager cache.  `outs`: optional (dWm, dbm,
-    dlog_std, dbz) tensors to write instead of fresh ones."""
+    dlog_std, dbz) tensors to write instead of fresh ones.  `reduce_stream`: the parameter
+    gradients' two reduce kernels run there (ordered after the row kernel on the current
+    stream, mepol_head_backward_phase), dz is ready on the current stream; the caller joins
+    reduce_stream before reading dWm / dbm / dlog_std / dbz (same bits either way).
+    `defer_reduce`: only the row kernel runs now; a sixth return value finish() launches the
+    reduces on the then-current stream, which must be ordered after this one and before the
+    workspace is reused."""
     import ctypes
 
     n, h = z.shape
@@ -367,9 +373,25 @@ def head_backward(grad_logp, z, Wm, log_std, act, mu, bz=None, need_dz=True, ws=
         dbm = torch.empty(a, dtype=torch.float64, device=dev)
         dls = torch.empty(a, dtype=torch.float64, device=dev)
         dbz = torch.empty(h, dtype=torch.float64, device=dev) if bz is not None else None
-    call("mepol_head_backward", ptr(grad_logp), ptr(z), n, h, ptr(bz), ptr(Wm), ptr(log_std),
-         ptr(act), ptr(mu), a, ptr(dz), ptr(dWm), ptr(dbm), ptr(dls), ptr(dbz), ptr(ws), ws.numel(),
-         _stream())
+    args = (ptr(grad_logp), ptr(z), n, h, ptr(bz), ptr(Wm), ptr(log_std), ptr(act), ptr(mu), a,
+            ptr(dz), ptr(dWm), ptr(dbm), ptr(dls), ptr(dbz), ptr(ws), ws.numel())
+    if defer_reduce:
+        call("mepol_head_backward_phase", *args, 1, _stream())
+        return dz, dWm, dbm, dls, dbz, lambda: call("mepol_head_backward_phase", *args, 2,
+                                                    _stream())
+    if reduce_stream is None:
+        call("mepol_head_backward", *args, _stream())
+        return dz, dWm, dbm, dls, dbz
+    call("mepol_head_backward_phase", *args, 1, _stream())
+    done = torch.cuda.Event()
+    done.record(torch.cuda.current_stream())
+    reduce_stream.wait_event(done)
+    with torch.cuda.stream(reduce_stream):
+        call("mepol_head_backward_phase", *args, 2, _stream())
+    if not torch.cuda.is_current_stream_capturing():  # a graph keeps its buffers alive
+        for t in (dWm, dbm, dls, dbz, ws):
+            if t is not None:
+                t.record_stream(reduce_stream)
     return dz, dWm, dbm, dls, dbz
 
 

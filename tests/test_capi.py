@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     for name in declared_functions():
         assert hasattr(lib, name), name
         assert name in _lib.SIGNATURES, f"{name} missing from the ctypes signature table"
-    assert lib.mepol_abi_version() == 3
+    assert lib.mepol_abi_version() == 4
 
 
 def test_nm_symbols_are_c_linkage():

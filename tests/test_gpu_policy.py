@@ -159,3 +159,31 @@ def test_weight_grad_matches_torch(cuda, n, o, i):
     # fixed-order sums: the same bits on a second call, with a caller-owned workspace too
     ws = ops.weight_grad_workspace(n, o, i, dy.device)
     assert torch.equal(ops.weight_grad(dy, x, ws=ws), out)
+
+
+@pytest.mark.parametrize("n,hidden,a", [(25000, 300, 8), (4099, 300, 17), (777, 64, 3)])
+def test_head_backward_phases_match_one_call(cuda, n, hidden, a):
+    """mepol_head_backward_phase: the row kernel on one stream and the parameter-gradient reduces
+    on another (as the off-policy iteration runs them) give the same bits as the one-call form."""
+    from mepol_amd import ops
+
+    g = torch.Generator(device="cuda").manual_seed(n)
+    f64 = dict(dtype=torch.float64, device="cuda")
+    z = torch.randn(n, hidden, generator=g, **f64)
+    bz = 0.1 * torch.randn(hidden, generator=g, **f64)
+    Wm = 0.05 * torch.randn(a, hidden, generator=g, **f64)
+    ls = torch.full((a,), -0.5, **f64)
+    act = torch.randn(n, a, generator=g, **f64)
+    mu = torch.randn(n, a, generator=g, **f64)
+    gl = torch.randn(n, generator=g, **f64)
+    ref = ops.head_backward(gl, z, Wm, ls, act, mu, bz=bz, need_dz=True)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    got = ops.head_backward(gl, z, Wm, ls, act, mu, bz=bz, need_dz=True, reduce_stream=side)
+    torch.cuda.current_stream().wait_stream(side)
+    *got2, finish = ops.head_backward(gl, z, Wm, ls, act, mu, bz=bz, need_dz=True,
+                                      defer_reduce=True)
+    finish()
+    torch.cuda.synchronize()
+    for r, t, t2 in zip(ref, got, got2):
+        assert torch.equal(r, t) and torch.equal(r, t2)
