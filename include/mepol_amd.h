@@ -251,6 +251,13 @@ int mepol_dh1_layer1_backward_masked(const double* dz2, int64_t n, int k, const 
                                      int hidden0, const uint16_t* h1_mask, const double* x,
                                      int in_features, double* dW1, double* db1, void* workspace,
                                      size_t workspace_bytes, void* stream);
+/* The masked form with the second Linear's weight as stored, W2 [k][hidden0] (hidden0 even,
+ * 16-B aligned), instead of W2^T: the kernel transposes its k-tiles on the way into LDS, so the
+ * caller needs no W2^T copy per optimizer step (ABI 4).  Identical results. */
+int mepol_dh1_layer1_backward_w2(const double* dz2, int64_t n, int k, const double* W2,
+                                 int hidden0, const uint16_t* h1_mask, const double* x,
+                                 int in_features, double* dW1, double* db1, void* workspace,
+                                 size_t workspace_bytes, void* stream);
 
 /* Weight gradient of a linear layer over a tall batch: dW [out, in] = dy^T x with dy [n, out]
  * and x [n, in] row-major f64 (the policy's dW2 = dz2^T h1, K = n), split-K on the f64 matrix

@@ -69,6 +69,8 @@ SIGNATURES = {
                                   _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_dh1_layer1_backward_masked": [_c_vp, _c_i64, _c_int, _c_vp, _c_int, _c_vp, _c_vp,
                                          _c_int, _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
+    "mepol_dh1_layer1_backward_w2": [_c_vp, _c_i64, _c_int, _c_vp, _c_int, _c_vp, _c_vp,
+                                     _c_int, _c_vp, _c_vp, _c_vp, _c_sz, _c_vp],
     "mepol_policy_forward_masked": [_c_vp, _c_i64, _c_int, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                                     _c_int, _c_vp, _c_vp, _c_vp, _c_vp, _c_int, _c_vp, _c_vp,
                                     _c_vp, _c_vp, _c_vp, _c_vp],

@@ -122,11 +122,15 @@ class DeviceIteration:
         self.fused_dh1 = (ops.dh1_layer1_ok(self.x.shape[1], W2.shape[0])
                           and os.environ.get("MEPOL_FUSED_DH1", "1") != "0")
         self.neg_one = torch.full((), -1.0, **f64)
-        self.W2t = torch.empty((W2.shape[1], W2.shape[0]), **f64) if self.fused_dh1 else None
         # relu'(h1) as bits, written by the fused forward beside h1 and read by the fused dh1
         # backward in place of h1 (1/64 of the bytes its epilogue waits for)
         self.h1_mask = (ops.h1_mask_buffer(self.N, W1.shape[0], dev)
                         if self.fused_fwd and self.fused_dh1 else None)
+        # W2^T only for the dh1 kernel without the mask or with an odd h0 (otherwise dh1 reads
+        # W2 as stored, mepol_dh1_layer1_backward_w2)
+        self.dh1_w2 = self.h1_mask is not None and W1.shape[0] % 2 == 0
+        self.W2t = (torch.empty((W2.shape[1], W2.shape[0]), **f64)
+                    if self.fused_dh1 and not self.dh1_w2 else None)
         # every body takes its optimizer step through _optim_step, which leaves theta_t in the
         # replay's shadow (off_policy_optimization then copies it into last_valid only when it
         # needs it, not after every accepted step)
@@ -299,11 +303,12 @@ class DeviceIteration:
         layer-1 backward, and than splitting dW2 across both phases)."""
         W1, b1, W2, b2, Wm, bm, ls = self.named
         cur = torch.cuda.current_stream()
-        # W2^T for the fused dh1 kernel, on this stream (measured: as a branch on the fork
-        # stream under the forward it delayed the forward's start by ~12 us, more than the copy)
-        if self.fused_dh1:
+        # W2^T for the fused dh1 kernel when it cannot read W2 as stored (round 6: with the
+        # forward's mask it does, mepol_dh1_layer1_backward_w2, and this copy node is gone)
+        w2_direct = self.fused_dh1 and self.dh1_w2
+        if self.fused_dh1 and not w2_direct:
             self.W2t.copy_(W2.t())
-        W2t = self.W2t if self.fused_dh1 else None
+        W2t = self.W2t if self.fused_dh1 and not w2_direct else None
         self.fork.wait_stream(cur)
         self.s_gemm.wait_stream(cur)
         o = outs if outs is not None else (None,) * 7
@@ -328,7 +333,8 @@ class DeviceIteration:
                 dh1 = None
                 dW1, db1 = ops.dh1_layer1_backward(dz2, W2t, self.h1, self.x, ws=self.ws_dh1,
                                                    mask=self.h1_mask,
-                                                   dW_out=o[0], db_out=o[1])
+                                                   dW_out=o[0], db_out=o[1],
+                                                   w2=W2 if w2_direct else None)
             else:
                 dh1 = torch.mm(dz2, W2)
                 dW1, db1 = ops.layer_backward(dh1, self.h1, self.x, ws=self.ws_layer)

@@ -56,7 +56,11 @@ struct Cfg {
 // LDS, after the MFMA block, so no select waits on a load right after issuing it.
 // DEEP: two register sets, the global loads of tile t + 2 issued while tile t is computed (the
 // store of tile t + 1 then waits on loads a whole tile older); 24 more VGPRs.
-template <int WR, int WC, int FR, int FC, bool DEEP = false>
+// BT: B given as [K][M] row-major (ldb = its row stride, M even, 16-B aligned rows): a lane loads
+// B[k][m, m + 1] (consecutive lanes consecutive m: coalesced) and writes the pair into LDS rows
+// m and m + 1 of the [BN][KT] image (two 8-B stores).  Lets dh1 = dz2 W2 read the Linear weight
+// as stored instead of a per-step W2^T copy.
+template <int WR, int WC, int FR, int FC, bool DEEP = false, bool BT = false>
 __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int64_t N, int K,
                                               int64_t lda, const double* __restrict__ B, int M,
                                               int64_t ldb, int64_t row0, int col0, double* lds,
@@ -82,9 +86,16 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
     }
 #pragma unroll
     for (int p = 0; p < P::PB; ++p) {
-      const int ch = min(tid + p * T, P::CB - 1), r = ch >> 3, k = kb + 2 * (ch & 7);
-      rb[p] = *reinterpret_cast<const double2*>(B + (int64_t)min(col0 + r, M - 1) * ldb +
-                                                min(k, k2));
+      const int ch = min(tid + p * T, P::CB - 1);
+      if constexpr (BT) {
+        const int kl = ch / (BN / 2), m = 2 * (ch % (BN / 2));
+        rb[p] = *reinterpret_cast<const double2*>(B + (int64_t)min(kb + kl, K - 1) * ldb +
+                                                  min(col0 + m, M - 2));
+      } else {
+        const int r = ch >> 3, k = kb + 2 * (ch & 7);
+        rb[p] = *reinterpret_cast<const double2*>(B + (int64_t)min(col0 + r, M - 1) * ldb +
+                                                  min(k, k2));
+      }
     }
   };
   auto lstore = [&](int kt, int buf, const RA& ra, const RB& rb) __attribute__((always_inline)) {
@@ -100,11 +111,21 @@ __device__ __forceinline__ void gemm_mainloop(const double* __restrict__ A, int6
     }
 #pragma unroll
     for (int p = 0; p < P::PB; ++p) {
-      const int ch = tid + p * T, r = ch >> 3, k = kb + 2 * (ch & 7);
+      const int ch = tid + p * T;
       if (ch < P::CB) {
-        const bool ok = col0 + r < M && k < K;
-        *reinterpret_cast<double2*>(sB + (buf * BN + r) * KP + 2 * lds_slot(r, ch & 7)) =
-            ok ? rb[p] : double2{0.0, 0.0};
+        if constexpr (BT) {
+          const int kl = ch / (BN / 2), m = 2 * (ch % (BN / 2));
+          const bool ok = col0 + m < M && kb + kl < K;  // M even: m + 1 < M with m
+          const int off = 2 * lds_slot(m, kl >> 1) + (kl & 1);  // rows m, m + 1: same swizzle
+          const int off1 = 2 * lds_slot(m + 1, kl >> 1) + (kl & 1);
+          sB[(buf * BN + m) * KP + off] = ok ? rb[p].x : 0.0;
+          sB[(buf * BN + m + 1) * KP + off1] = ok ? rb[p].y : 0.0;
+        } else {
+          const int r = ch >> 3, k = kb + 2 * (ch & 7);
+          const bool ok = col0 + r < M && k < K;
+          *reinterpret_cast<double2*>(sB + (buf * BN + r) * KP + 2 * lds_slot(r, ch & 7)) =
+              ok ? rb[p] : double2{0.0, 0.0};
+        }
       }
     }
   };
@@ -233,7 +254,8 @@ using P = Cfg<WR, WC, FR, FC>;
 // h1[r][16 kt + b] > 0 in bit b, mepol_policy_forward_masked) instead of the f64 h1 values:
 // 2 B per 16 columns instead of 128 B, which the epilogue waited for with the MFMAs idle
 // (one workgroup per CU).  The same bits either way.
-template <int NH, bool MASK>  // NH = ceil((F + 1) / 16) column groups of [x | 1]
+// BT: W2t is the Linear weight W2 as stored, [K][M] (gemm_mainloop's BT)
+template <int NH, bool MASK, bool BT>  // NH = ceil((F + 1) / 16) column groups of [x | 1]
 __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
     const double* __restrict__ dz2, int64_t N, int K, const double* __restrict__ W2t, int M,
     const void* __restrict__ h1v, const double* __restrict__ x, int F,
@@ -249,7 +271,8 @@ __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
   const int64_t row0 = (int64_t)rb * BM;
   const int col0 = (tile % ncb) * BN;
   d4 acc[FR][FC];
-  gemm_mainloop<WR, WC, FR, FC, true>(dz2, N, K, K, W2t, M, K, row0, col0, lds, acc);
+  gemm_mainloop<WR, WC, FR, FC, true, BT>(dz2, N, K, K, W2t, M, BT ? M : K, row0, col0, lds,
+                                         acc);
 
   // Every epilogue operand in ONE batch of unconditional loads (clamped addresses) before the
   // first use: the ReLU mask of h1 at the wave's accumulator elements and the [x | 1] operands.
@@ -441,7 +464,7 @@ extern "C" int mepol_dh1_layer1_workspace_size(int64_t n, int m, int in_features
   return 0;
 }
 
-template <bool MASK>
+template <bool MASK, bool BT = false>
 static int dh1_layer1_backward(const double* dz2, int64_t n, int k, const double* W2t, int m,
                                const void* h1, const double* x, int in_features, double* dW1,
                                double* db1, void* workspace, size_t workspace_bytes,
@@ -450,7 +473,7 @@ static int dh1_layer1_backward(const double* dz2, int64_t n, int k, const double
   using mepol::gemm::dh1_layer1_bwd_kernel;
   const int F = in_features;
   if (n <= 0 || k <= 0 || (k & 1) || m <= 0 || F <= 0 || F > 63 || !dz2 || !W2t || !h1 || !x ||
-      !dW1 || !workspace || ((uintptr_t)dz2 & 15) || ((uintptr_t)W2t & 15)) {
+      !dW1 || !workspace || ((uintptr_t)dz2 & 15) || ((uintptr_t)W2t & 15) || (BT && (m & 1))) {
     mepol::set_error("mepol_dh1_layer1_backward: bad arguments (k even, in_features <= 63, "
                      "16-B aligned dz2 / W2t)");
     return mepol::kErrBadArg;
@@ -470,11 +493,11 @@ static int dh1_layer1_backward(const double* dz2, int64_t n, int k, const double
   do {                                                                                         \
     static bool attr = false;                                                                  \
     if (!attr) {                                                                               \
-      MEPOL_HIP(hipFuncSetAttribute((const void*)dh1_layer1_bwd_kernel<NHV, MASK>,             \
+      MEPOL_HIP(hipFuncSetAttribute((const void*)dh1_layer1_bwd_kernel<NHV, MASK, BT>,         \
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)P::kLds)); \
       attr = true;                                                                             \
     }                                                                                          \
-    hipLaunchKernelGGL((dh1_layer1_bwd_kernel<NHV, MASK>), dim3(tiles), dim3(P::kThreads),      \
+    hipLaunchKernelGGL((dh1_layer1_bwd_kernel<NHV, MASK, BT>), dim3(tiles), dim3(P::kThreads),  \
                        P::kLds, st,                                                            \
                        dz2, n, k, W2t, m, h1, x, F, part);                                     \
   } while (0)
@@ -514,4 +537,13 @@ extern "C" int mepol_dh1_layer1_backward_masked(const double* dz2, int64_t n, in
                                                 void* stream) {
   return dh1_layer1_backward<true>(dz2, n, k, W2t, m, h1_mask, x, in_features, dW1, db1,
                                    workspace, workspace_bytes, stream);
+}
+
+extern "C" int mepol_dh1_layer1_backward_w2(const double* dz2, int64_t n, int k, const double* W2,
+                                            int m, const uint16_t* h1_mask, const double* x,
+                                            int in_features, double* dW1, double* db1,
+                                            void* workspace, size_t workspace_bytes,
+                                            void* stream) {
+  return dh1_layer1_backward<true, true>(dz2, n, k, W2, m, h1_mask, x, in_features, dW1, db1,
+                                         workspace, workspace_bytes, stream);
 }

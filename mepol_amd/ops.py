@@ -445,13 +445,20 @@ def dh1_layer1_ok(in_features, hidden1):
     return in_features <= DH1_L1_MAX_IN and hidden1 % 2 == 0
 
 
-def dh1_layer1_backward(dz2, W2t, h1, x, ws=None, dW_out=None, db_out=None, mask=None):
+def dh1_layer1_backward(dz2, W2t, h1, x, ws=None, dW_out=None, db_out=None, mask=None,
+                        w2=None):
     """(dW1, db1) of h1 = relu(x W1^T + b1) from dz2 = dL/dz2 [n, h1w] and W2t = W2^T
-    [h0, h1w]: dh1 = dz2 W2 is reduced on chip (csrc/gemm.hip), never written."""
+    [h0, h1w]: dh1 = dz2 W2 is reduced on chip (csrc/gemm.hip), never written.  With `w2`
+    (W2 as stored, [h1w, h0]; needs `mask`) W2t is not read and may be None: the kernel
+    transposes W2's tiles itself (mepol_dh1_layer1_backward_w2)."""
     n, k = dz2.shape
-    h0 = W2t.shape[0]
     f = x.shape[1]
-    assert W2t.shape[1] == k and h1.shape == (n, h0) and dz2.is_contiguous() and W2t.is_contiguous()
+    if w2 is not None:
+        h0 = w2.shape[1]
+        assert mask is not None and w2.shape[0] == k and w2.is_contiguous() and dz2.is_contiguous()
+    else:
+        h0 = W2t.shape[0]
+        assert W2t.shape[1] == k and h1.shape == (n, h0) and dz2.is_contiguous() and W2t.is_contiguous()
     if ws is None:
         import ctypes
 
@@ -462,7 +469,11 @@ def dh1_layer1_backward(dz2, W2t, h1, x, ws=None, dW_out=None, db_out=None, mask
                                                       device=x.device)
     db = db_out if db_out is not None else torch.empty(h0, dtype=torch.float64, device=x.device)
     assert dW.is_contiguous() and db.is_contiguous()
-    if mask is None:
+    if w2 is not None:
+        assert mask.shape == (n, (h0 + 15) // 16) and mask.dtype == torch.int16
+        call("mepol_dh1_layer1_backward_w2", ptr(dz2), n, k, ptr(w2), h0, ptr(mask), ptr(x), f,
+             ptr(dW), ptr(db), ptr(ws), ws.numel(), _stream())
+    elif mask is None:
         call("mepol_dh1_layer1_backward", ptr(dz2), n, k, ptr(W2t), h0, ptr(h1), ptr(x), f,
              ptr(dW), ptr(db), ptr(ws), ws.numel(), _stream())
     else:  # relu'(h1) from the forward's bit mask (policy_forward(mask_out=...))

@@ -81,3 +81,6 @@ def test_h1_mask_and_masked_dh1(cuda, n, nf, h0, h1w, a):
     dW1, db1 = ops.dh1_layer1_backward(dz2, W2t, h1, x)
     dW1m, db1m = ops.dh1_layer1_backward(dz2, W2t, h1, x, mask=mask)
     assert torch.equal(dW1, dW1m) and torch.equal(db1, db1m)
+    if h0 % 2 == 0:  # W2 as stored, transposed on the way into LDS (mepol_dh1_layer1_backward_w2)
+        dW1w, db1w = ops.dh1_layer1_backward(dz2, None, h1, x, mask=mask, w2=W2)
+        assert torch.equal(dW1, dW1w) and torch.equal(db1, db1w)

@@ -3,7 +3,7 @@
 set -o pipefail
 out=gpurun_out/$1; mkdir -p "$out"
 timeout -k 10 900 python -u -m pytest -x -q --timeout 400 --timeout-method thread \
-  tests/test_gpu_policy.py tests/test_gpu_device_loop.py tests/test_gpu_sharded_graph.py tests/test_gpu_sharded_world2.py \
+  tests/test_gpu_gemm.py tests/test_gpu_policy.py tests/test_gpu_device_loop.py tests/test_gpu_sharded_graph.py tests/test_gpu_sharded_world2.py \
   tests/test_gpu_sharded_world2_distinct.py tests/test_gpu_reference_caller.py \
   tests/test_gpu_distributed.py > "$out/tests.log" 2>&1
 rc=$?; tail -3 "$out/tests.log"; [ $rc = 0 ] || exit $rc
