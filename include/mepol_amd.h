@@ -143,7 +143,9 @@ int mepol_csr_build(const int32_t* idxT, int64_t nq, int k, int64_t col_offset, 
                     int64_t row_offset, int32_t* csr_off, int32_t* csr_rows, void* workspace,
                     size_t workspace_bytes, void* stream);
 /* gamma_j = sum_{i in CSR(j)} g_i ; partials[b] = block sums of gamma_j w_j: partials holds
- * min(ceil(16 n_own / 256), 2048) doubles (16 lanes per particle, grid-stride beyond). */
+ * mepol_entropy_gamma_partials_size(n_own) doubles = min(ceil(8 n_own / 256), 2048) (8 lanes
+ * per particle since ABI 4, grid-stride beyond). */
+int mepol_entropy_gamma_partials_size(int64_t n_own);
 int mepol_entropy_gamma(const double* g, const double* w_own, const int32_t* csr_off,
                         const int32_t* csr_rows, int64_t n_own, double* gamma_out,
                         double* partials, void* stream);

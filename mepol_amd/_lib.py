@@ -35,6 +35,7 @@ SIGNATURES = {
                          _c_vp],
     "mepol_iw_normalize": [_c_vp, _c_vp, _c_i64, _c_vp, _c_vp],
     "mepol_entropy_partials_size": [_c_i64],
+    "mepol_entropy_gamma_partials_size": [_c_i64],
     "mepol_entropy_forward": [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_dbl, _c_dbl,
                               _c_dbl, _c_dbl, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp],
     "mepol_entropy_forward_emit": [_c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_int, _c_int, _c_dbl, _c_dbl,

@@ -375,6 +375,11 @@ extern "C" int mepol_entropy_forward_emit(const double* w, const int32_t* idxT, 
                               out4, vals, stream);
 }
 
+// The block partials mepol_entropy_gamma writes for n_own particles (its reverse scan reads them).
+extern "C" int mepol_entropy_gamma_partials_size(int64_t n_own) {
+  return (int)std::min<int64_t>((n_own * kGammaLanes + 255) / 256, kGammaMaxBlocks);
+}
+
 // gamma over the n_own particles this rank owns (CSR over its own ids), partial S per block.
 extern "C" int mepol_entropy_gamma(const double* g, const double* w_own, const int32_t* csr_off,
                                    const int32_t* csr_rows, int64_t n_own, double* gamma_out,

@@ -309,9 +309,9 @@ def csr_build(idxT, k, n_own, col_offset=0, row_offset=0, nq=None):
 
 
 def entropy_gamma_nparts(n_own):
-    """Block partials entropy_gamma returns: one per 256-thread block (16 lanes per particle),
-    at most 2048 blocks (csrc/entropy.hip)."""
-    return min((n_own * 16 + 255) // 256, 2048)
+    """Block partials entropy_gamma returns (csrc/entropy.hip: one per 256-thread block of
+    kGammaLanes lanes per particle, at most kGammaMaxBlocks)."""
+    return int(_lib.load().mepol_entropy_gamma_partials_size(n_own))
 
 
 def entropy_gamma(g, w_own, csr_off, csr_rows):

@@ -9,7 +9,7 @@ shift 2
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp
 for kv in "" "$@"; do
-  tag=${kv:-default}; tag=${tag//=/_}
+  tag=${kv:-default}; tag=${tag##*/}; tag=${tag//=/_}
   ( [ -n "$kv" ] && export "$kv"; timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv \
     -d $out/tr_${w}_$tag -o run -- python3 $root/bench.py --workload $w --steps 2 --warmup 1 \
     --no-cpu-baseline > $out/bench_${w}_$tag.json 2> $out/bench_${w}_$tag.err ) \
