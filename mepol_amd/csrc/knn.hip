@@ -262,6 +262,47 @@ __device__ __forceinline__ double exact_d2_pad_pre(const float (&qa)[32],
   return s;
 }
 
+// Lane l's value from lane l ^ M: DPP quad permutes for M = 1, 2 (a VALU move), ds_swizzle's
+// xor mode for M = 4 .. 16 (no address operand), ds_bpermute (__shfl_xor) for M = 32.
+template <int M>
+__device__ __forceinline__ int xor_lane(int v) {
+  if constexpr (M == 1)
+    return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);  // quad_perm [1, 0, 3, 2]
+  else if constexpr (M == 2)
+    return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, false);  // quad_perm [2, 3, 0, 1]
+  else if constexpr (M < 32)
+    return __builtin_amdgcn_ds_swizzle(v, 0x1F | (M << 10));  // and 31, or 0, xor M
+  else
+    return __shfl_xor(v, M, kWave);
+}
+template <int M>
+__device__ __forceinline__ double xor_lane(double x) {
+  const int2 v = __builtin_bit_cast(int2, x);
+  return __builtin_bit_cast(double, make_int2(xor_lane<M>(v.x), xor_lane<M>(v.y)));
+}
+
+// One compare-exchange stage of the ascending bitonic sort of 64 (d, i) pairs across the wave.
+template <int SIZE, int STRIDE>
+__device__ __forceinline__ void bitonic_stage(double& dd, int& di, int l) {
+  const double od = xor_lane<STRIDE>(dd);
+  const int oi = xor_lane<STRIDE>(di);
+  const bool up = (l & SIZE) == 0;
+  const bool lower = (l & STRIDE) == 0;
+  const bool other_less = lex_less(od, oi, dd, di);
+  // lower lane keeps the min if ascending block, max otherwise
+  const bool take = (lower == up) ? other_less : !other_less && !(od == dd && oi == di);
+  if (take) {
+    dd = od;
+    di = oi;
+  }
+  if constexpr (STRIDE > 1) bitonic_stage<SIZE, STRIDE / 2>(dd, di, l);
+}
+template <int SIZE = 2>
+__device__ __forceinline__ void bitonic_sort64(double& dd, int& di, int l) {
+  bitonic_stage<SIZE, SIZE / 2>(dd, di, l);
+  if constexpr (SIZE < 64) bitonic_sort64<SIZE * 2>(dd, di, l);
+}
+
 template <int LIST, int MAXP>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void refine_kernel(
     const float* __restrict__ cpad, int dp, int64_t nc, const float* __restrict__ query,
@@ -453,24 +494,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
       di = c;
     }
   }
-  // Bitonic sort of 64 (dd, di) pairs across the wave, ascending.
-#pragma unroll
-  for (int size = 2; size <= 64; size <<= 1) {
-#pragma unroll
-    for (int stride = size >> 1; stride >= 1; stride >>= 1) {
-      const double od = __shfl_xor(dd, stride, kWave);
-      const int oi = __shfl_xor(di, stride, kWave);
-      const bool up = ((l & size) == 0);
-      const bool lower = ((l & stride) == 0);
-      const bool other_less = lex_less(od, oi, dd, di);
-      // lower lane keeps the min if ascending block, max otherwise
-      const bool take = (lower == up) ? other_less : !other_less && !(od == dd && oi == di);
-      if (take) {
-        dd = od;
-        di = oi;
-      }
-    }
-  }
+  // Bitonic sort of 64 (dd, di) pairs across the wave, ascending (the same network as the
+  // round-5 __shfl_xor loop; the partner exchanges by DPP / ds_swizzle where the stride allows)
+  bitonic_sort64(dd, di, l);
   // Certification: every candidate outside the exactly evaluated set has exact
   // d^2 >= bnd + |q|^2 - E.
   const double ek = __shfl(dd, kp1 - 1, kWave);
