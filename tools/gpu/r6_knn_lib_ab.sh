@@ -14,7 +14,7 @@ for v in new old new old; do
   echo "$v: $(grep 'knn ms' $out/$v.log)"
 done
 cd /tmp && export TMPDIR=/tmp
-for v in new old; do
+for v in ${ORDER:-new old}; do
   if [ $v = old ]; then export MEPOL_AMD_LIB=$root/$2; else unset MEPOL_AMD_LIB; fi
   timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$root/$out/prof_$v" -o run -- \
     python3 "$root/tools/knn_probe.py" --reps 3 $CFG > "$root/$out/prof_$v.log" 2>&1 || exit 1
