@@ -319,41 +319,56 @@ __global__ __launch_bounds__(l1b::P::kThreads) void dh1_layer1_bwd_kernel(
         xb[i][q][h] = fma(xb[i][q][h], keep, one);
       }
     }
-  double* red = lds;  // [WR][NH][4][64]: the main loop's last barrier retired its LDS reads
+  // The wave partials of JB column fragments per LDS round (2 when they fit beside each other:
+  // 6 workgroup barriers instead of 10 for FC = 5); the per-element sum over the WR waves keeps
+  // its order.  The main loop's last barrier retired its LDS reads.
   constexpr int NE = NH * 4 * 64;
+  constexpr int JB = 2 * WR * NE * sizeof(double) <= P::kLds ? 2 : 1;
+  double* red = lds;  // [JB][WR][NH][4][64]
 #pragma unroll
-  for (int j = 0; j < FC; ++j) {
-    const int c = col0 + j * 16 + fr;
-    d4 dacc[NH];
+  for (int j0 = 0; j0 < FC; j0 += JB) {
 #pragma unroll
-    for (int h = 0; h < NH; ++h) dacc[h] = d4{0.0, 0.0, 0.0, 0.0};
+    for (int jj = 0; jj < JB; ++jj) {
+      const int j = j0 + jj;
+      if (j < FC) {
+        const int c = col0 + j * 16 + fr;
+        d4 dacc[NH];
 #pragma unroll
-    for (int i = 0; i < FR; ++i)
+        for (int h = 0; h < NH; ++h) dacc[h] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        bool on;
-        if constexpr (MASK)
-          on = ((hv[j][i][q] >> fr) & 1u) != 0;
-        else
-          on = hv[j][i][q] > 0.0;
-        const double dz = (on && c < M) ? acc[i][j][q] : 0.0;
+        for (int i = 0; i < FR; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            bool on;
+            if constexpr (MASK)
+              on = ((hv[j][i][q] >> fr) & 1u) != 0;
+            else
+              on = hv[j][i][q] > 0.0;
+            const double dz = (on && c < M) ? acc[i][j][q] : 0.0;
+#pragma unroll
+            for (int h = 0; h < NH; ++h)
+              dacc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(dz, xb[i][q][h], dacc[h], 0, 0, 0);
+          }
+        // dacc[h][r'] = sum over the wave's rows of dz1[.][col0 + 16 j + g + 4 r'] *
+        // [x|1][16 h + fr]
 #pragma unroll
         for (int h = 0; h < NH; ++h)
-          dacc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(dz, xb[i][q][h], dacc[h], 0, 0, 0);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            red[(jj * WR + wave) * NE + (h * 4 + q) * 64 + lane] = dacc[h][q];
       }
-    // dacc[h][r'] = sum over the wave's rows of dz1[.][col0 + 16 j + g + 4 r'] * [x|1][16 h + fr]
-#pragma unroll
-    for (int h = 0; h < NH; ++h)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) red[((wave * NH + h) * 4 + q) * 64 + lane] = dacc[h][q];
+    }
     __syncthreads();
-    for (int e = threadIdx.x; e < NE; e += T) {
-      double s = red[e];
+    for (int e = threadIdx.x; e < JB * NE; e += T) {
+      const int jj = e / NE, ee = e - jj * NE, j = j0 + jj;
+      if (j < FC) {
+        double s = red[jj * WR * NE + ee];
 #pragma unroll
-      for (int w = 1; w < WR; ++w) s += red[w * NE + e];
-      const int l = e & 63, q = (e >> 6) & 3, h = e >> 8;
-      const int cc = col0 + j * 16 + (l >> 4) + 4 * q, f = 16 * h + (l & 15);
-      if (cc < M && f <= F) part[((int64_t)rb * M + cc) * (F + 1) + f] = s;
+        for (int w = 1; w < WR; ++w) s += red[(jj * WR + w) * NE + ee];
+        const int l = ee & 63, q = (ee >> 6) & 3, h = ee >> 8;
+        const int cc = col0 + j * 16 + (l >> 4) + 4 * q, f = 16 * h + (l & 15);
+        if (cc < M && f <= F) part[((int64_t)rb * M + cc) * (F + 1) + f] = s;
+      }
     }
     __syncthreads();
   }
